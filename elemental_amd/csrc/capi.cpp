@@ -1,0 +1,287 @@
+// extern "C" boundary (include/elemental_amd.h).  Every entry point runs
+// inside Guard(), which turns the C++ exceptions into ELX_ERR_* codes.
+#include "common.hpp"
+#include "runtime/runtime.hpp"
+#include "comm/comm.hpp"
+#include "core/distmatrix.hpp"
+#include "core/redist.hpp"
+#include "core/gemm.hpp"
+#include "core/exec.hpp"
+#include <string>
+
+struct elx_comm_s { std::shared_ptr<elx::Comm> c; };
+struct elx_grid_s { std::shared_ptr<elx::Grid> g; };
+struct elx_dm_s { std::shared_ptr<elx::DistMatrix> m; };
+
+namespace elx {
+namespace {
+thread_local std::string g_last_error;
+
+Dist ToDist(int d) {
+    if (d < ELX_MC || d > ELX_CIRC) throw LogicError(Cat("invalid dist ", d));
+    return static_cast<Dist>(d);
+}
+Device ToDevice(int d) {
+    if (d != ELX_DEVICE_CPU && d != ELX_DEVICE_GPU) throw LogicError(Cat("invalid device ", d));
+    return static_cast<Device>(d);
+}
+DistMatrix& M(elx_dm_t h) {
+    if (!h || !h->m) throw LogicError("null DistMatrix handle");
+    return *h->m;
+}
+void CheckOp(int o) {
+    if (o != ELX_NORMAL && o != ELX_TRANSPOSE && o != ELX_ADJOINT) throw LogicError(Cat("invalid orientation ", o));
+}
+hipStream_t S(void* s) { return Runtime::Get().Resolve(s); }
+}  // namespace
+
+void SetLastError(const std::string& msg) { g_last_error = msg; }
+}  // namespace elx
+
+using namespace elx;
+
+extern "C" {
+
+const char* elx_last_error(void) { return g_last_error.c_str(); }
+int elx_version(void) { return 10000; }
+
+int elx_device_count(int* count) {
+    return Guard([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        *count = n;
+    });
+}
+int elx_set_device(int device) { return Guard([&] { Runtime::Get().SetDevice(device); Runtime::Get().EnsureGPU(); }); }
+int elx_get_device(int* device) { return Guard([&] { Runtime::Get().EnsureGPU(); *device = Runtime::Get().DeviceId(); }); }
+int elx_device_synchronize(void) {
+    return Guard([&] { Runtime::Get().EnsureGPU(); ELX_CHECK_HIP(hipDeviceSynchronize()); });
+}
+int elx_default_stream(void** stream) { return Guard([&] { *stream = Runtime::Get().ComputeStream(); }); }
+int elx_stream_create(void** stream) {
+    return Guard([&] {
+        Runtime::Get().EnsureGPU();
+        hipStream_t s;
+        ELX_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *stream = s;
+    });
+}
+int elx_stream_destroy(void* stream) { return Guard([&] { ELX_CHECK_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream))); }); }
+int elx_stream_synchronize(void* stream) { return Guard([&] { ELX_CHECK_HIP(hipStreamSynchronize(S(stream))); }); }
+
+int elx_pool_alloc(void** ptr, size_t bytes, void* stream) {
+    return Guard([&] { *ptr = Runtime::Get().Alloc(bytes, S(stream)); });
+}
+int elx_pool_free(void* ptr, void* stream) { return Guard([&] { Runtime::Get().Free(ptr, S(stream)); }); }
+int elx_pool_trim(size_t keep) { return Guard([&] { Runtime::Get().Trim(keep); }); }
+int elx_pool_stats(size_t* reserved, size_t* in_use) { return Guard([&] { Runtime::Get().Stats(*reserved, *in_use); }); }
+int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    return Guard([&] {
+        hipStream_t s = S(stream);
+        ELX_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+    });
+}
+int elx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    return Guard([&] {
+        hipStream_t s = S(stream);
+        ELX_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+    });
+}
+int elx_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+    return Guard([&] { ELX_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream))); });
+}
+
+// ---- local GEMM ----------------------------------------------------------
+#define ELX_GEMM_ENTRY(NAME, DT, ST, SC)                                                              \
+    int NAME(int opA, int opB, int64_t m, int64_t n, int64_t k, SC alpha, const ST* A, int64_t lda,    \
+             const ST* B, int64_t ldb, SC beta, ST* C, int64_t ldc, void* stream) {                  \
+        return Guard([&] {                                                                             \
+            CheckOp(opA);                                                                              \
+            CheckOp(opB);                                                                              \
+            ELX_REQUIRE(m >= 0 && n >= 0 && k >= 0, "negative GEMM dimension");                       \
+            const bool ta = opA != ELX_NORMAL, tb = opB != ELX_NORMAL;                                 \
+            ELX_REQUIRE(ldc >= (m > 1 ? m : 1), "ldc too small");                                     \
+            ELX_REQUIRE(lda >= ((ta ? k : m) > 1 ? (ta ? k : m) : 1), "lda too small");               \
+            ELX_REQUIRE(ldb >= ((tb ? n : k) > 1 ? (tb ? n : k) : 1), "ldb too small");               \
+            if (m == 0 || n == 0) return;                                                              \
+            exec::Gemm(Device::GPU, DT, ta, tb, m, n, k, (double)alpha, A, lda, B, ldb, (double)beta, C, \
+                       ldc, S(stream));                                                                \
+        });                                                                                            \
+    }
+ELX_GEMM_ENTRY(elx_gemm_f64, DType::F64, double, double)
+ELX_GEMM_ENTRY(elx_gemm_f32, DType::F32, float, float)
+ELX_GEMM_ENTRY(elx_gemm_f16, DType::F16, uint16_t, float)
+ELX_GEMM_ENTRY(elx_gemm_bf16, DType::BF16, uint16_t, float)
+#undef ELX_GEMM_ENTRY
+
+// ---- BLAS-1 --------------------------------------------------------------
+int elx_axpy2d(int dtype, int64_t m, int64_t n, double alpha, const void* X, int64_t xcs, int64_t xrs, void* Y,
+               int64_t ycs, int64_t yrs, void* stream) {
+    return Guard([&] {
+        kern::Copy2D d{m, n, X, xcs, xrs, Y, ycs, yrs};
+        exec::Copy2DBatch(Device::GPU, ToDType(dtype), &d, 1, true, alpha, S(stream));
+    });
+}
+int elx_copy2d(int dtype, int64_t m, int64_t n, const void* A, int64_t acs, int64_t ars, void* B, int64_t bcs,
+               int64_t brs, void* stream) {
+    return Guard([&] {
+        kern::Copy2D d{m, n, A, acs, ars, B, bcs, brs};
+        exec::Copy2DBatch(Device::GPU, ToDType(dtype), &d, 1, false, 0.0, S(stream));
+    });
+}
+int elx_transpose(int dtype, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb, void* stream) {
+    return Guard([&] {  // B (n x m) = A^T
+        kern::Copy2D d{n, m, A, lda, 1, B, 1, ldb};
+        exec::Copy2DBatch(Device::GPU, ToDType(dtype), &d, 1, false, 0.0, S(stream));
+    });
+}
+int elx_scale2d(int dtype, int64_t m, int64_t n, double alpha, void* A, int64_t lda, void* stream) {
+    return Guard([&] { exec::Scale(Device::GPU, ToDType(dtype), m, n, alpha, A, lda, S(stream)); });
+}
+int elx_fill2d(int dtype, int64_t m, int64_t n, double value, void* A, int64_t lda, void* stream) {
+    return Guard([&] { exec::Fill(Device::GPU, ToDType(dtype), m, n, value, A, lda, S(stream)); });
+}
+int elx_hadamard2d(int dtype, int64_t m, int64_t n, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                   int64_t ldc, void* stream) {
+    return Guard([&] { exec::Hadamard(Device::GPU, ToDType(dtype), m, n, A, lda, B, ldb, C, ldc, S(stream)); });
+}
+int elx_entrywise_map(int dtype, int fn, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb,
+                      void* stream) {
+    return Guard([&] { exec::Map(Device::GPU, ToDType(dtype), fn, m, n, A, lda, B, ldb, S(stream)); });
+}
+int elx_fill_hash(int dtype, int64_t m, int64_t n, void* A, int64_t lda, int64_t i0, int64_t istride, int64_t j0,
+                  int64_t jstride, uint64_t seed, double center, double radius, void* stream) {
+    return Guard([&] {
+        exec::FillHash(Device::GPU, ToDType(dtype), m, n, A, lda, i0, istride, j0, jstride, seed, center, radius,
+                       S(stream));
+    });
+}
+
+// ---- communication ---------------------------------------------------------
+int elx_comm_unique_id(unsigned char id[128]) {
+    return Guard([&] {
+        ncclUniqueId uid;
+        ncclResult_t r = ncclGetUniqueId(&uid);
+        if (r != ncclSuccess) throw CommError(Cat("ncclGetUniqueId: ", ncclGetErrorString(r)));
+        std::memcpy(id, uid.internal, 128);
+    });
+}
+int elx_comm_init_rccl(elx_comm_t* world, int rank, int size, const unsigned char id[128]) {
+    return Guard([&] { *world = new elx_comm_s{Comm::InitRCCL(rank, size, id)}; });
+}
+int elx_comm_init_host(elx_comm_t* world, int rank, int size, elx_host_coll_fn coll, elx_host_split_fn split,
+                       void* ctx) {
+    return Guard([&] {
+        *world = new elx_comm_s{size == 1 && !coll ? Comm::Self() : Comm::InitHost(rank, size, coll, split, ctx)};
+    });
+}
+int elx_comm_rank(elx_comm_t c, int* rank) { return Guard([&] { *rank = c->c->Rank(); }); }
+int elx_comm_size(elx_comm_t c, int* size) { return Guard([&] { *size = c->c->Size(); }); }
+int elx_comm_destroy(elx_comm_t c) { return Guard([&] { delete c; }); }
+int elx_comm_allgather(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
+    return Guard([&] {
+        const Device d = c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU;
+        c->c->AllGather(ToDType(dtype), send, recv, count, d, d == Device::GPU ? S(stream) : nullptr);
+    });
+}
+int elx_comm_reduce_scatter(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
+    return Guard([&] {
+        const Device d = c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU;
+        c->c->ReduceScatter(ToDType(dtype), send, recv, count, d, d == Device::GPU ? S(stream) : nullptr);
+    });
+}
+int elx_comm_barrier(elx_comm_t c) { return Guard([&] { c->c->Barrier(); }); }
+int elx_comm_stats(int64_t* bytes, double* seconds, int64_t* calls) {
+    return Guard([&] {
+        auto& s = GlobalCommStats();
+        *bytes = s.bytes;
+        *seconds = s.seconds;
+        *calls = s.calls;
+    });
+}
+int elx_comm_stats_reset(void) { return Guard([&] { GlobalCommStats() = CommStats{}; }); }
+
+// ---- grid ----------------------------------------------------------------------
+int elx_grid_default_height(int size) { return size > 0 ? Grid::DefaultHeight(size) : 0; }
+int elx_grid_create(elx_grid_t* grid, elx_comm_t world, int height, int order) {
+    return Guard([&] {
+        ELX_REQUIRE(world && world->c, "null comm");
+        ELX_REQUIRE(order == ELX_ROW_MAJOR || order == ELX_COLUMN_MAJOR, "bad grid order");
+        *grid = new elx_grid_s{std::make_shared<Grid>(world->c, height, order)};
+    });
+}
+int elx_grid_info(elx_grid_t g, int* info) {
+    return Guard([&] {
+        const Grid& G = *g->g;
+        int v[8] = {G.Height(), G.Width(), G.Size(), G.Rank(), G.MCRank(), G.MRRank(), G.VCRank(), G.VRRank()};
+        std::memcpy(info, v, sizeof(v));
+    });
+}
+int elx_grid_destroy(elx_grid_t g) { return Guard([&] { delete g; }); }
+
+// ---- DistMatrix ------------------------------------------------------------------
+int elx_dm_create(elx_dm_t* A, elx_grid_t g, int dtype, int coldist, int rowdist, int device, int root) {
+    return Guard([&] {
+        ELX_REQUIRE(g && g->g, "null grid");
+        *A = new elx_dm_s{std::make_shared<DistMatrix>(g->g, ToDType(dtype), ToDist(coldist), ToDist(rowdist),
+                                                       ToDevice(device), root)};
+    });
+}
+int elx_dm_destroy(elx_dm_t A) { return Guard([&] { delete A; }); }
+int elx_dm_align(elx_dm_t A, int ca, int ra, int constrain) { return Guard([&] { M(A).Align(ca, ra, constrain != 0); }); }
+int elx_dm_align_with(elx_dm_t A, elx_dm_t B, int constrain) { return Guard([&] { M(A).AlignWith(M(B), constrain != 0); }); }
+int elx_dm_resize(elx_dm_t A, int64_t h, int64_t w) { return Guard([&] { M(A).Resize(h, w); }); }
+int elx_dm_info(elx_dm_t A, int64_t* info) {
+    return Guard([&] {
+        const DistMatrix& X = M(A);
+        const bool p = X.Participating();
+        int64_t v[13] = {X.Height(), X.Width(), X.LocalHeight(), X.LocalWidth(), X.LDim(), X.ColAlign(),
+                         X.RowAlign(), p ? X.ColShift() : 0, p ? X.RowShift() : 0, X.ColStride(), X.RowStride(),
+                         p ? 1 : 0, X.Viewing() ? 1 : 0};
+        std::memcpy(info, v, sizeof(v));
+    });
+}
+int elx_dm_buffer(elx_dm_t A, void** ptr) { return Guard([&] { *ptr = M(A).Buffer(); }); }
+int elx_dm_set_local(elx_dm_t A, const void* host, int64_t ld) { return Guard([&] { M(A).SetLocal(host, ld); }); }
+int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld) { return Guard([&] { M(A).GetLocal(host, ld); }); }
+int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1) {
+    return Guard([&] { *V = new elx_dm_s{DistMatrix::View(M(A), i0, i1, j0, j1)}; });
+}
+int elx_dm_copy(elx_dm_t B, elx_dm_t A) { return Guard([&] { Copy(M(A), M(B)); }); }
+int elx_dm_transpose(elx_dm_t A, elx_dm_t B) { return Guard([&] { Transpose(M(A), M(B)); }); }
+int elx_dm_fill_hash(elx_dm_t A, uint64_t seed, double center, double radius) {
+    return Guard([&] { M(A).FillHash(seed, center, radius); });
+}
+int elx_dm_synchronize(elx_dm_t A) { return Guard([&] { M(A).Synchronize(); }); }
+
+int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y) { return Guard([&] { Axpy(alpha, M(X), M(Y)); }); }
+int elx_dm_scale(double alpha, elx_dm_t A) { return Guard([&] { Scale(alpha, M(A)); }); }
+int elx_dm_zero(elx_dm_t A) { return Guard([&] { Zero(M(A)); }); }
+int elx_dm_hadamard(elx_dm_t A, elx_dm_t B, elx_dm_t C) { return Guard([&] { Hadamard(M(A), M(B), M(C)); }); }
+int elx_dm_entrywise_map(int fn, elx_dm_t A, elx_dm_t B) { return Guard([&] { EntrywiseMap(fn, M(A), M(B)); }); }
+int elx_dm_axpy_contract(double alpha, elx_dm_t A, elx_dm_t B) { return Guard([&] { AxpyContract(alpha, M(A), M(B)); }); }
+
+int elx_gemm(int oA, int oB, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C, int alg) {
+    return Guard([&] {
+        CheckOp(oA);
+        CheckOp(oB);
+        ELX_REQUIRE(alg >= ELX_GEMM_DEFAULT && alg <= ELX_GEMM_CANNON, "invalid GemmAlgorithm ", alg);
+        Gemm(oA, oB, alpha, M(A), M(B), beta, M(C), alg);
+    });
+}
+int elx_local_gemm(int oA, int oB, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C) {
+    return Guard([&] {
+        CheckOp(oA);
+        CheckOp(oB);
+        LocalGemm(oA == ELX_NORMAL ? ELX_NORMAL : ELX_TRANSPOSE, oB == ELX_NORMAL ? ELX_NORMAL : ELX_TRANSPOSE, alpha,
+                  M(A), M(B), beta, M(C));
+    });
+}
+int elx_set_blocksize(int64_t nb) { return Guard([&] { SetBlocksize(nb); }); }
+int64_t elx_blocksize(void) { return Blocksize(); }
+int elx_set_compute_panel(int64_t kc) { return Guard([&] { SetComputePanel(kc); }); }
+int elx_last_gemm_algorithm(void) { return LastGemmAlgorithm(); }
+
+}  // extern "C"

@@ -1,0 +1,268 @@
+#include "comm.hpp"
+#include <chrono>
+#include <cstring>
+#include <algorithm>
+
+namespace elx {
+
+CommStats& GlobalCommStats() {
+    static CommStats s;
+    return s;
+}
+
+namespace {
+
+ncclDataType_t NcclType(DType t) {
+    switch (t) {
+    case DType::F32: return ncclFloat32;
+    case DType::F64: return ncclFloat64;
+    case DType::F16: return ncclFloat16;
+    case DType::BF16: return ncclBfloat16;
+    }
+    throw LogicError("bad dtype");
+}
+
+void CheckNccl(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw CommError(Cat("RCCL ", what, " failed: ", ncclGetErrorString(r)));
+}
+
+void CopyBytes(Device dev, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0 || dst == src) return;
+    if (dev == Device::GPU) ELX_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    else std::memcpy(dst, src, bytes);
+}
+
+// Pinned staging buffer for host-backend collectives on device data.
+struct Staging {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* Get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) (void)hipHostFree(p);
+            ELX_CHECK_HIP(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return p;
+    }
+};
+
+}  // namespace
+
+std::shared_ptr<Comm> Comm::Self() {
+    auto c = std::shared_ptr<Comm>(new Comm());
+    c->kind_ = Kind::SELF;
+    return c;
+}
+
+std::shared_ptr<Comm> Comm::InitRCCL(int rank, int size, const unsigned char id[128]) {
+    Runtime::Get().EnsureGPU();
+    ncclUniqueId uid;
+    static_assert(sizeof(uid.internal) == 128, "ncclUniqueId size");
+    std::memcpy(uid.internal, id, 128);
+    auto c = std::shared_ptr<Comm>(new Comm());
+    c->kind_ = Kind::RCCL;
+    c->rank_ = rank;
+    c->size_ = size;
+    CheckNccl(ncclCommInitRank(&c->nccl_, size, uid, rank), "ncclCommInitRank");
+    return c;
+}
+
+std::shared_ptr<Comm> Comm::InitHost(int rank, int size, elx_host_coll_fn coll, elx_host_split_fn split, void* ctx) {
+    ELX_REQUIRE(coll != nullptr, "host comm needs a collective callback");
+    ELX_REQUIRE(rank >= 0 && rank < size, "bad rank ", rank, " of ", size);
+    auto c = std::shared_ptr<Comm>(new Comm());
+    c->kind_ = Kind::HOST;
+    c->rank_ = rank;
+    c->size_ = size;
+    c->coll_ = coll;
+    c->split_ = split;
+    c->ctx_ = ctx;
+    c->group_ = 0;
+    return c;
+}
+
+Comm::~Comm() {
+    if (nccl_) (void)ncclCommDestroy(nccl_);
+}
+
+std::shared_ptr<Comm> Comm::Split(int color, int key) {
+    if (kind_ == Kind::SELF) return Self();
+    auto c = std::shared_ptr<Comm>(new Comm());
+    c->kind_ = kind_;
+    if (kind_ == Kind::RCCL) {
+        CheckNccl(ncclCommSplit(nccl_, color, key, &c->nccl_, nullptr), "ncclCommSplit");
+        CheckNccl(ncclCommUserRank(c->nccl_, &c->rank_), "ncclCommUserRank");
+        CheckNccl(ncclCommCount(c->nccl_, &c->size_), "ncclCommCount");
+        return c;
+    }
+    ELX_REQUIRE(split_ != nullptr, "host comm has no split callback");
+    ELX_REQUIRE(group_ == 0, "host comm: only the world communicator can be split");
+    int g = 0, r = 0, sz = 1;
+    if (split_(ctx_, group_, color, key, &g, &r, &sz) != 0) throw CommError("host split callback failed");
+    c->coll_ = coll_;
+    c->split_ = split_;
+    c->ctx_ = ctx_;
+    c->group_ = g;
+    c->rank_ = r;
+    c->size_ = sz;
+    return c;
+}
+
+void Comm::HostCall(int op, DType t, const void* send, void* recv, Int count, int peer, int peer2) {
+    auto t0 = std::chrono::steady_clock::now();
+    const int rc = coll_(ctx_, op, group_, static_cast<int>(t), send, recv, count, peer, peer2);
+    GlobalCommStats().seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != 0) throw CommError(Cat("host collective op ", op, " failed with ", rc));
+}
+
+void Comm::AllGather(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+    const size_t es = DTypeSize(t), bytes = static_cast<size_t>(count) * es;
+    auto& st = GlobalCommStats();
+    st.calls++;
+    st.bytes += static_cast<int64_t>(bytes) * (size_ - 1);
+    if (size_ == 1) { CopyBytes(dev, recv, send, bytes, s); return; }
+    if (count == 0) return;
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        CheckNccl(ncclAllGather(send, recv, count, NcclType(t), nccl_, s), "ncclAllGather");
+        return;
+    }
+    if (dev == Device::CPU) { HostCall(ELX_COLL_ALLGATHER, t, send, recv, count, 0, 0); return; }
+    static Staging stg;
+    char* h = static_cast<char*>(stg.Get(bytes * (size_ + 1)));
+    ELX_CHECK_HIP(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+    HostCall(ELX_COLL_ALLGATHER, t, h, h + bytes, count, 0, 0);
+    ELX_CHECK_HIP(hipMemcpyAsync(recv, h + bytes, bytes * size_, hipMemcpyHostToDevice, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+    const size_t es = DTypeSize(t), bytes = static_cast<size_t>(count) * es;
+    auto& st = GlobalCommStats();
+    st.calls++;
+    st.bytes += static_cast<int64_t>(bytes) * (size_ - 1);
+    if (size_ == 1) { CopyBytes(dev, recv, send, bytes, s); return; }
+    if (count == 0) return;
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclReduceScatter");
+        return;
+    }
+    if (dev == Device::CPU) { HostCall(ELX_COLL_REDUCE_SCATTER, t, send, recv, count, 0, 0); return; }
+    static Staging stg;
+    char* h = static_cast<char*>(stg.Get(bytes * (size_ + 1)));
+    ELX_CHECK_HIP(hipMemcpyAsync(h, send, bytes * size_, hipMemcpyDeviceToHost, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+    HostCall(ELX_COLL_REDUCE_SCATTER, t, h, h + bytes * size_, count, 0, 0);
+    ELX_CHECK_HIP(hipMemcpyAsync(recv, h + bytes * size_, bytes, hipMemcpyHostToDevice, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+    const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
+    if (size_ == 1) { CopyBytes(dev, recv, send, bytes, s); return; }
+    if (count == 0) return;
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclAllReduce");
+        return;
+    }
+    if (dev == Device::CPU) { HostCall(ELX_COLL_ALLREDUCE, t, send, recv, count, 0, 0); return; }
+    static Staging stg;
+    char* h = static_cast<char*>(stg.Get(bytes * 2));
+    ELX_CHECK_HIP(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+    HostCall(ELX_COLL_ALLREDUCE, t, h, h + bytes, count, 0, 0);
+    ELX_CHECK_HIP(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+void Comm::Bcast(DType t, void* buf, Int count, int root, Device dev, hipStream_t s) {
+    const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
+    if (size_ == 1 || count == 0) return;
+    GlobalCommStats().calls++;
+    if (rank_ != root) GlobalCommStats().bytes += static_cast<int64_t>(bytes);
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        CheckNccl(ncclBroadcast(buf, buf, count, NcclType(t), root, nccl_, s), "ncclBroadcast");
+        return;
+    }
+    if (dev == Device::CPU) { HostCall(ELX_COLL_BCAST, t, buf, buf, count, root, 0); return; }
+    static Staging stg;
+    char* h = static_cast<char*>(stg.Get(bytes));
+    ELX_CHECK_HIP(hipMemcpyAsync(h, buf, bytes, hipMemcpyDeviceToHost, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+    HostCall(ELX_COLL_BCAST, t, h, h, count, root, 0);
+    ELX_CHECK_HIP(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, const std::vector<Int>& sd, void* recv,
+                     const std::vector<Int>& rc, const std::vector<Int>& rd, Device dev, hipStream_t s) {
+    const size_t es = DTypeSize(t);
+    const char* sb = static_cast<const char*>(send);
+    char* rb = static_cast<char*>(recv);
+    auto& st = GlobalCommStats();
+    st.calls++;
+    for (int q = 0; q < size_; ++q)
+        if (q != rank_) st.bytes += static_cast<int64_t>(rc[q] * es);
+    // the self portion never leaves the device
+    CopyBytes(dev, rb + rd[rank_] * es, sb + sd[rank_] * es, static_cast<size_t>(rc[rank_]) * es, s);
+    if (size_ == 1) return;
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        const ncclDataType_t nt = NcclType(t);
+        CheckNccl(ncclGroupStart(), "ncclGroupStart");
+        for (int q = 0; q < size_; ++q) {
+            if (q == rank_) continue;
+            if (sc[q] > 0) CheckNccl(ncclSend(sb + sd[q] * es, sc[q], nt, q, nccl_, s), "ncclSend");
+            if (rc[q] > 0) CheckNccl(ncclRecv(rb + rd[q] * es, rc[q], nt, q, nccl_, s), "ncclRecv");
+        }
+        CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+        return;
+    }
+    // host backend: uniform-count all-to-all padded to the largest pair
+    std::vector<int64_t> mine(sc.begin(), sc.end()), all(static_cast<size_t>(size_) * size_);
+    {
+        // gather every rank's send-count vector as doubles (exact for counts < 2^53)
+        std::vector<double> md(mine.begin(), mine.end()), ad(all.size());
+        HostCall(ELX_COLL_ALLGATHER, DType::F64, md.data(), ad.data(), size_, 0, 0);
+        for (size_t i = 0; i < ad.size(); ++i) all[i] = static_cast<int64_t>(ad[i]);
+    }
+    const Int maxc = *std::max_element(all.begin(), all.end());
+    if (maxc == 0) return;
+    const size_t pb = static_cast<size_t>(maxc) * es;
+    std::vector<char> hs(pb * size_), hr(pb * size_);
+    if (dev == Device::GPU) ELX_CHECK_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < size_; ++q) {
+        if (q == rank_ || sc[q] == 0) continue;
+        if (dev == Device::GPU)
+            ELX_CHECK_HIP(hipMemcpy(hs.data() + q * pb, sb + sd[q] * es, sc[q] * es, hipMemcpyDeviceToHost));
+        else
+            std::memcpy(hs.data() + q * pb, sb + sd[q] * es, sc[q] * es);
+    }
+    HostCall(ELX_COLL_ALLTOALL, t, hs.data(), hr.data(), maxc, 0, 0);
+    for (int q = 0; q < size_; ++q) {
+        if (q == rank_ || rc[q] == 0) continue;
+        if (dev == Device::GPU)
+            ELX_CHECK_HIP(hipMemcpy(rb + rd[q] * es, hr.data() + q * pb, rc[q] * es, hipMemcpyHostToDevice));
+        else
+            std::memcpy(rb + rd[q] * es, hr.data() + q * pb, rc[q] * es);
+    }
+}
+
+void Comm::Barrier() {
+    if (size_ == 1) return;
+    if (kind_ == Kind::RCCL) {
+        hipStream_t s = Runtime::Get().CommStream();
+        static Buffer flag;
+        if (!flag.data()) flag.Reset(Device::GPU, 64, nullptr);
+        CheckNccl(ncclAllReduce(flag.data(), flag.data(), 1, ncclFloat32, ncclSum, nccl_, s), "barrier");
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    HostCall(ELX_COLL_BARRIER, DType::F32, nullptr, nullptr, 0, 0, 0);
+}
+
+}  // namespace elx

@@ -1,0 +1,72 @@
+// Communication backend: replaces the reference's El::mpi collective overload
+// sets and their Aluminum/NCCL glue (src/core/imports/mpi/{AllGather,ReduceScatter,
+// AllToAll,SendRecv,Broadcast}.hpp, include/El/core/imports/aluminum.hpp:24-365).
+//
+//   * RCCL (device buffers): one communicator per grid dimension, built with
+//     ncclCommSplit from the world communicator; collectives are enqueued on the
+//     caller's HIP stream (never host-blocking, unlike the reference's plain-MPI
+//     path which calls hipStreamSynchronize before every collective,
+//     src/core/imports/mpi/AllGather.hpp:36).  Irregular exchanges are grouped
+//     ncclSend/ncclRecv: on xGMI every peer pair has its own link, so a direct
+//     exchange uses c-1 links at once instead of one ring neighbour.
+//   * HOST (host buffers): the caller supplies the collective as a callback
+//     (e.g. torch.distributed/gloo); device buffers are staged through pinned
+//     host memory.  Used by the CPU multi-rank tests.
+//   * SELF: size-1 communicator, every collective is a local copy.
+#pragma once
+#include "../common.hpp"
+#include "../runtime/runtime.hpp"
+#include <memory>
+#include <vector>
+#include <rccl/rccl.h>
+
+namespace elx {
+
+struct CommStats {
+    int64_t bytes = 0;   // algorithmic bytes received by this rank
+    int64_t calls = 0;
+    double seconds = 0;  // host wall time spent inside host-backend collectives
+};
+CommStats& GlobalCommStats();
+
+class Comm {
+public:
+    enum class Kind { SELF, RCCL, HOST };
+
+    static std::shared_ptr<Comm> Self();
+    static std::shared_ptr<Comm> InitRCCL(int rank, int size, const unsigned char id[128]);
+    static std::shared_ptr<Comm> InitHost(int rank, int size, elx_host_coll_fn coll, elx_host_split_fn split,
+                                          void* ctx);
+    ~Comm();
+
+    Kind kind() const { return kind_; }
+    int Rank() const { return rank_; }
+    int Size() const { return size_; }
+    // Collective over this comm: ranks with equal color form a new comm ordered by key.
+    std::shared_ptr<Comm> Split(int color, int key);
+
+    // All counts are in elements of `t`; `dev` says where the buffers live.
+    void AllGather(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
+    void ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
+    void AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
+    void Bcast(DType t, void* buf, Int count, int root, Device dev, hipStream_t s);
+    // Irregular all-to-all: sendcounts/recvcounts per peer (elements), with
+    // element displacements into send/recv.  Pairs with zero count are skipped.
+    void AllToAllV(DType t, const void* send, const std::vector<Int>& scounts, const std::vector<Int>& sdispls,
+                   void* recv, const std::vector<Int>& rcounts, const std::vector<Int>& rdispls, Device dev,
+                   hipStream_t s);
+    void Barrier();
+
+private:
+    Comm() = default;
+    void HostCall(int op, DType t, const void* send, void* recv, Int count, int peer, int peer2);
+    Kind kind_ = Kind::SELF;
+    int rank_ = 0, size_ = 1;
+    ncclComm_t nccl_ = nullptr;
+    elx_host_coll_fn coll_ = nullptr;
+    elx_host_split_fn split_ = nullptr;
+    void* ctx_ = nullptr;
+    int group_ = 0;
+};
+
+}  // namespace elx

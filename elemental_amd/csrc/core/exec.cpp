@@ -1,0 +1,222 @@
+#include "exec.hpp"
+#include "../kernels/elem.hpp"
+#include <cmath>
+#include <vector>
+
+namespace elx {
+namespace exec {
+
+namespace {
+
+// Host element access in the compute type of each dtype (f16/bf16 -> float).
+template <typename S> struct H;
+template <> struct H<double> {
+    using C = double;
+    static C ld(const double* p) { return *p; }
+    static void st(double* p, C v) { *p = v; }
+};
+template <> struct H<float> {
+    using C = float;
+    static C ld(const float* p) { return *p; }
+    static void st(float* p, C v) { *p = v; }
+};
+struct Half16 { uint16_t b; };
+struct Brain16 { uint16_t b; };
+template <> struct H<Half16> {
+    using C = float;
+    static C ld(const Half16* p) { return HalfToFloat(p->b); }
+    static void st(Half16* p, C v) { p->b = FloatToHalf(v); }
+};
+template <> struct H<Brain16> {
+    using C = float;
+    static C ld(const Brain16* p) { return BF16ToFloat(p->b); }
+    static void st(Brain16* p, C v) { p->b = FloatToBF16(v); }
+};
+
+#define HOST_DTYPE_SWITCH(t, S, ...)                                   \
+    switch (t) {                                                       \
+    case DType::F64: { using S = double; __VA_ARGS__; break; }         \
+    case DType::F32: { using S = float; __VA_ARGS__; break; }          \
+    case DType::F16: { using S = Half16; __VA_ARGS__; break; }         \
+    case DType::BF16: { using S = Brain16; __VA_ARGS__; break; }       \
+    }
+
+template <typename S>
+void cpu_copy(const Copy2D& d, bool axpy, double alpha) {
+    const S* src = static_cast<const S*>(d.src);
+    S* dst = static_cast<S*>(d.dst);
+    using C = typename H<S>::C;
+    const C a = (C)alpha;
+    for (Int j = 0; j < d.n; ++j)
+        for (Int i = 0; i < d.m; ++i) {
+            const S* x = src + i * d.scs + j * d.srs;
+            S* y = dst + i * d.dcs + j * d.drs;
+            if (axpy) H<S>::st(y, H<S>::ld(y) + a * H<S>::ld(x));
+            else *y = *x;
+        }
+}
+
+template <typename S>
+void cpu_gemm(bool ta, bool tb, Int m, Int n, Int k, double alpha, const S* A, Int lda, const S* B,
+              Int ldb, double beta, S* C, Int ldc) {
+    using Cm = typename H<S>::C;
+    std::vector<Cm> acc(static_cast<size_t>(m));
+    for (Int j = 0; j < n; ++j) {
+        std::fill(acc.begin(), acc.end(), Cm(0));
+        for (Int l = 0; l < k; ++l) {
+            const Cm b = H<S>::ld(tb ? B + j + l * ldb : B + l + j * ldb);
+            if (b == Cm(0)) continue;
+            if (!ta) {
+                const S* acol = A + l * lda;
+                for (Int i = 0; i < m; ++i) acc[i] += H<S>::ld(acol + i) * b;
+            } else {
+                for (Int i = 0; i < m; ++i) acc[i] += H<S>::ld(A + l + i * lda) * b;
+            }
+        }
+        for (Int i = 0; i < m; ++i) {
+            S* c = C + i + j * ldc;
+            const Cm v = (Cm)alpha * acc[i];
+            H<S>::st(c, beta == 0.0 ? v : v + (Cm)beta * H<S>::ld(c));
+        }
+    }
+}
+
+template <typename Cm>
+Cm cpu_map(int fn, Cm x) {
+    switch (fn) {
+    case ELX_MAP_IDENTITY: return x;
+    case ELX_MAP_NEGATE: return -x;
+    case ELX_MAP_ABS: return std::fabs(x);
+    case ELX_MAP_SQUARE: return x * x;
+    case ELX_MAP_SQRT: return std::sqrt(x);
+    case ELX_MAP_EXP: return std::exp(x);
+    case ELX_MAP_LOG: return std::log(x);
+    case ELX_MAP_RELU: return x > Cm(0) ? x : Cm(0);
+    case ELX_MAP_SIGMOID: return Cm(1) / (Cm(1) + std::exp(-x));
+    case ELX_MAP_RECIP: return Cm(1) / x;
+    case ELX_MAP_TANH: return std::tanh(x);
+    default: throw LogicError(Cat("unknown entrywise functor ", fn));
+    }
+}
+
+void check(hipError_t e, const char* what) {
+    if (e != hipSuccess)
+        throw HIPError(Cat(what, ": ", hipGetErrorName(e), " (", hipGetErrorString(e), ")"));
+}
+
+}  // namespace
+
+void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s) {
+    if (nd <= 0) return;
+    if (dev == Device::GPU) {
+        check(kern::copy2d_batch(static_cast<int>(t), d, nd, axpy, alpha, s), "copy2d_batch");
+        return;
+    }
+    for (int q = 0; q < nd; ++q) HOST_DTYPE_SWITCH(t, S, cpu_copy<S>(d[q], axpy, alpha));
+}
+
+void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alpha, const void* A, Int lda,
+          const void* B, Int ldb, double beta, void* C, Int ldc, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) {
+        hipError_t e = hipSuccess;
+        switch (t) {
+        case DType::F64:
+            e = kern::gemm_mfma<double>(ta, tb, m, n, k, alpha, static_cast<const double*>(A), lda,
+                                        static_cast<const double*>(B), ldb, beta, static_cast<double*>(C), ldc, s);
+            break;
+        case DType::F32:
+            e = kern::gemm_mfma<float>(ta, tb, m, n, k, (float)alpha, static_cast<const float*>(A), lda,
+                                       static_cast<const float*>(B), ldb, (float)beta, static_cast<float*>(C),
+                                       ldc, s);
+            break;
+        case DType::F16:
+        case DType::BF16:
+            e = kern::gemm_mfma_h(t == DType::BF16, ta, tb, m, n, k, (float)alpha,
+                                  static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb,
+                                  (float)beta, static_cast<uint16_t*>(C), ldc, s);
+            break;
+        }
+        check(e, "gemm_mfma");
+        return;
+    }
+    HOST_DTYPE_SWITCH(t, S,
+        cpu_gemm<S>(ta, tb, m, n, k, alpha, static_cast<const S*>(A), lda, static_cast<const S*>(B), ldb, beta,
+                    static_cast<S*>(C), ldc));
+}
+
+void Fill(Device dev, DType t, Int m, Int n, double v, void* A, Int lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) { check(kern::fill2d((int)t, m, n, v, A, lda, s), "fill2d"); return; }
+    HOST_DTYPE_SWITCH(t, S, {
+        S* a = static_cast<S*>(A);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) H<S>::st(a + i + j * lda, (typename H<S>::C)v);
+    });
+}
+
+void Scale(Device dev, DType t, Int m, Int n, double alpha, void* A, Int lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) { check(kern::scale2d((int)t, m, n, alpha, A, lda, s), "scale2d"); return; }
+    HOST_DTYPE_SWITCH(t, S, {
+        S* a = static_cast<S*>(A);
+        using Cm = typename H<S>::C;
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) H<S>::st(a + i + j * lda, (Cm)alpha * H<S>::ld(a + i + j * lda));
+    });
+}
+
+void Hadamard(Device dev, DType t, Int m, Int n, const void* A, Int lda, const void* B, Int ldb, void* C,
+              Int ldc, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) { check(kern::hadamard2d((int)t, m, n, A, lda, B, ldb, C, ldc, s), "hadamard2d"); return; }
+    HOST_DTYPE_SWITCH(t, S, {
+        const S* a = static_cast<const S*>(A);
+        const S* b = static_cast<const S*>(B);
+        S* c = static_cast<S*>(C);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i)
+                H<S>::st(c + i + j * ldc, H<S>::ld(a + i + j * lda) * H<S>::ld(b + i + j * ldb));
+    });
+}
+
+void Map(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s) {
+    if (fn < ELX_MAP_IDENTITY || fn > ELX_MAP_TANH) throw LogicError(Cat("unknown entrywise functor ", fn));
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) { check(kern::entrywise_map((int)t, fn, m, n, A, lda, B, ldb, s), "entrywise_map"); return; }
+    HOST_DTYPE_SWITCH(t, S, {
+        const S* a = static_cast<const S*>(A);
+        S* b = static_cast<S*>(B);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) H<S>::st(b + i + j * ldb, cpu_map(fn, H<S>::ld(a + i + j * lda)));
+    });
+}
+
+void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
+              uint64_t seed, double center, double radius, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) {
+        check(kern::fill_hash((int)t, m, n, A, lda, i0, is, j0, js, seed, center, radius, s), "fill_hash");
+        return;
+    }
+    HOST_DTYPE_SWITCH(t, S, {
+        S* a = static_cast<S*>(A);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) {
+                const double u = kern::hash_unit(seed, i0 + i * is, j0 + j * js);
+                H<S>::st(a + i + j * lda, (typename H<S>::C)(center + radius * (2.0 * u - 1.0)));
+            }
+    });
+}
+
+double LoadScalar(DType t, const void* p) {
+    double v = 0;
+    HOST_DTYPE_SWITCH(t, S, v = (double)H<S>::ld(static_cast<const S*>(p)));
+    return v;
+}
+void StoreScalar(DType t, void* p, double v) {
+    HOST_DTYPE_SWITCH(t, S, H<S>::st(static_cast<S*>(p), (typename H<S>::C)v));
+}
+
+}  // namespace exec
+}  // namespace elx

@@ -1,0 +1,31 @@
+// Device-dispatched local primitives.  Device::GPU launches the gfx950 kernels
+// (elemental_amd/csrc/kernels); Device::CPU runs the host loops that back the
+// reference's Device::CPU DistMatrix path (used when a caller builds CPU
+// matrices, e.g. the gloo multi-rank tests).  A GPU matrix never runs here on
+// the host: there is no fallback between the two.
+#pragma once
+#include "../common.hpp"
+#include "../runtime/runtime.hpp"
+#include "../kernels/kernels.hpp"
+
+namespace elx {
+namespace exec {
+
+using kern::Copy2D;
+
+void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
+void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alpha,
+          const void* A, Int lda, const void* B, Int ldb, double beta, void* C, Int ldc, hipStream_t s);
+void Fill(Device dev, DType t, Int m, Int n, double v, void* A, Int lda, hipStream_t s);
+void Scale(Device dev, DType t, Int m, Int n, double alpha, void* A, Int lda, hipStream_t s);
+void Hadamard(Device dev, DType t, Int m, Int n, const void* A, Int lda, const void* B, Int ldb,
+              void* C, Int ldc, hipStream_t s);
+void Map(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s);
+void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
+              uint64_t seed, double center, double radius, hipStream_t s);
+// host-side scalar conversion of one element (for Get/Set and tests)
+double LoadScalar(DType t, const void* p);
+void StoreScalar(DType t, void* p, double v);
+
+}  // namespace exec
+}  // namespace elx

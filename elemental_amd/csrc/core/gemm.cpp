@@ -1,0 +1,385 @@
+// SUMMA drivers for El::Gemm on DistMatrices.
+//
+// Mirrors src/blas_like/level3/Gemm.cpp:273-302 (front door: Scale(beta,C) then
+// dispatch on orientation) and src/blas_like/level3/Gemm/{NN,NT,TN,TT}.hpp
+// (A-, B-, C-stationary and Dot variants + the 2/10 weight heuristic).
+//
+// What is MI355X-specific:
+//  * C-stationary (the hot path, configs C1/C2/C3): every panel gather is a
+//    single-hop redistribution (redist.cpp) straight into the layout the local
+//    MFMA update reads ([MC,*] and [*,MR] for NN - no transpose pass), enqueued
+//    on a dedicated high-priority comm stream into one of two panel slots while
+//    the MFMA kernel consumes the other slot on the compute stream (event
+//    fenced both ways).  This is what the reference's off-by-default
+//    multistream variants approximate (NN_Multistream.hpp:262-412) without
+//    their S extra copies of C.
+//  * communication panel (Blocksize(), default 128) and compute panel are
+//    decoupled: ComputePanel() consecutive columns of A / rows of B are moved
+//    per step (default 2048, whole k on a 1x1 grid where the "gathers" are
+//    local views), so the fp64 update runs at k >= 2048 instead of k = 128 and
+//    C's HBM round trip per panel stays a few % of the MFMA time.  Only the
+//    summation order changes (normwise tolerance); data movement is bit-exact.
+//  * the _MS algorithm ids run the same pipelined variants (the reference's
+//    ROCm build rejects NT/TN _MS, TN.hpp:124-128).
+#include "gemm.hpp"
+#include "redist.hpp"
+#include "exec.hpp"
+#include <algorithm>
+
+namespace elx {
+
+namespace {
+Int g_blocksize = 128;      // src/core/environment.cpp:315
+Int g_compute_panel = 0;    // 0 = automatic
+int g_last_alg = ELX_GEMM_DEFAULT;
+constexpr Int kDotBlock = 2000;  // NN.hpp:578 (hard-coded in the reference)
+
+bool IsN(int o) { return o == ELX_NORMAL; }
+
+void FenceStreams(hipStream_t from, hipStream_t to) {
+    if (!from || !to || from == to) return;
+    hipEvent_t ev;
+    ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ELX_CHECK_HIP(hipEventRecord(ev, from));
+    ELX_CHECK_HIP(hipStreamWaitEvent(to, ev, 0));
+    ELX_CHECK_HIP(hipEventDestroy(ev));
+}
+
+// DistMatrixReadProxy: A itself when it already has dist (cd,rd) [and the
+// requested alignment], else a redistributed copy.
+std::shared_ptr<const DistMatrix> ReadProxy(const DistMatrix& A, Dist cd, Dist rd, int calign = -1,
+                                            int ralign = -1) {
+    const bool ok = A.ColDist() == cd && A.RowDist() == rd && (calign < 0 || A.ColAlign() == calign) &&
+                    (ralign < 0 || A.RowAlign() == ralign);
+    if (ok) return std::shared_ptr<const DistMatrix>(&A, [](const DistMatrix*) {});
+    auto T = A.Like(cd, rd);
+    if (calign >= 0) T->AlignCols(calign, true);
+    if (ralign >= 0) T->AlignRows(ralign, true);
+    Copy(A, *T);
+    return T;
+}
+
+// DistMatrixReadWriteProxy for C: work in [MC,MR]; copy back on Finish().
+struct RWProxy {
+    DistMatrix& orig;
+    std::shared_ptr<DistMatrix> tmp;
+    explicit RWProxy(DistMatrix& C) : orig(C) {
+        if (C.ColDist() != Dist::MC || C.RowDist() != Dist::MR) {
+            tmp = C.Like(Dist::MC, Dist::MR);
+            Copy(C, *tmp);
+        }
+    }
+    DistMatrix& Get() { return tmp ? *tmp : orig; }
+    void Finish() { if (tmp) Copy(*tmp, orig); }
+};
+
+void Check(bool cond, const char* what) {
+    if (!cond) throw LogicError(Cat("LocalGemm: ", what));
+}
+
+Int EffectivePanel(const Grid& g, Int K) {
+    const Int nb = std::max<Int>(1, g_blocksize);
+    Int kc = g_compute_panel;
+    if (kc <= 0) kc = (g.Size() == 1) ? K : std::max<Int>(nb, 2048);
+    kc = std::max<Int>(nb, (kc + nb - 1) / nb * nb);  // whole communication panels
+    return std::max<Int>(1, kc);
+}
+
+// ---------------------------------------------------------------------------
+// C-stationary SUMMA, all four orientations (NN.hpp:341-385, NT.hpp:251-294,
+// TN.hpp:252-291, TT.hpp:195-240), pipelined over two panel slots.
+//   op(A) panel: NORMAL -> A(:,k) as [MC,*];   TRANSPOSE -> A(k,:) as [*,MC]
+//   op(B) panel: NORMAL -> B(k,:) as [*,MR];   TRANSPOSE -> B(:,k) as [MR,*]
+// ---------------------------------------------------------------------------
+void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    RWProxy Cp(CPre);
+    const DistMatrix& A = *Ap;
+    const DistMatrix& B = *Bp;
+    DistMatrix& C = Cp.Get();
+    const Int K = IsN(oA) ? A.Width() : A.Height();
+    const Grid& g = C.G();
+    const Device dev = C.Dev();
+    const bool gpu = dev == Device::GPU;
+    hipStream_t cs = C.Stream();
+    hipStream_t ms = gpu ? Runtime::Get().CommStream() : nullptr;
+    const Int kc = EffectivePanel(g, K);
+    const Dist a_cd = IsN(oA) ? Dist::MC : Dist::STAR, a_rd = IsN(oA) ? Dist::STAR : Dist::MC;
+    const Dist b_cd = IsN(oB) ? Dist::STAR : Dist::MR, b_rd = IsN(oB) ? Dist::MR : Dist::STAR;
+
+    // inputs (and beta*C) must be complete before the comm stream reads them
+    if (gpu) {
+        FenceStreams(A.Stream(), ms);
+        FenceStreams(B.Stream(), ms);
+        FenceStreams(cs, ms);
+    }
+
+    struct Slot {
+        std::shared_ptr<DistMatrix> a, b;                 // gathered panels (owned temporaries)
+        std::shared_ptr<const DistMatrix> ua, ub;         // what the update reads (temporary or view)
+        hipEvent_t ready = nullptr, done = nullptr;
+        bool pending = false;                             // done recorded, not yet waited by comm
+    } slot[2];
+    for (auto& s : slot) {
+        s.a = A.Like(a_cd, a_rd);
+        s.b = B.Like(b_cd, b_rd);
+        s.a->SetStream(ms);
+        s.b->SetStream(ms);
+        // AlignWith(C): A1 rows follow C's rows, B1 cols follow C's cols
+        if (IsN(oA)) s.a->AlignCols(C.ColAlign(), true); else s.a->AlignRows(C.ColAlign(), true);
+        if (IsN(oB)) s.b->AlignRows(C.RowAlign(), true); else s.b->AlignCols(C.RowAlign(), true);
+        if (gpu) {
+            ELX_CHECK_HIP(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming));
+            ELX_CHECK_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        }
+    }
+    const int np = static_cast<int>((K + kc - 1) / kc);
+
+    auto issue = [&](int p) {
+        Slot& s = slot[p & 1];
+        const Int k0 = p * kc, k1 = std::min(K, k0 + kc);
+        if (gpu && s.pending) ELX_CHECK_HIP(hipStreamWaitEvent(ms, s.done, 0));
+        auto Av = IsN(oA) ? DistMatrix::View(A, 0, A.Height(), k0, k1) : DistMatrix::View(A, k0, k1, 0, A.Width());
+        auto Bv = IsN(oB) ? DistMatrix::View(B, k0, k1, 0, B.Width()) : DistMatrix::View(B, 0, B.Height(), k0, k1);
+        Av->SetStream(ms);
+        Bv->SetStream(ms);
+        // a panel whose local block already IS the gathered layout (e.g. every
+        // panel on a 1x1 grid) is used in place: no copy at all
+        if (SameLocalLayout(*Av, a_cd, a_rd, s.a->ColAlign(), s.a->RowAlign())) s.ua = Av;
+        else { Copy(*Av, *s.a); s.ua = s.a; }
+        if (SameLocalLayout(*Bv, b_cd, b_rd, s.b->ColAlign(), s.b->RowAlign())) s.ub = Bv;
+        else { Copy(*Bv, *s.b); s.ub = s.b; }
+        if (gpu) ELX_CHECK_HIP(hipEventRecord(s.ready, ms));
+    };
+    auto compute = [&](int p) {
+        Slot& s = slot[p & 1];
+        const DistMatrix& a = *s.ua;
+        const DistMatrix& b = *s.ub;
+        if (gpu) ELX_CHECK_HIP(hipStreamWaitEvent(cs, s.ready, 0));
+        const Int m = C.LocalHeight(), n = C.LocalWidth();
+        const Int k = IsN(oA) ? a.LocalWidth() : a.LocalHeight();
+        if (m > 0 && n > 0 && k > 0)
+            exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(), b.LDim(),
+                       1.0, C.Buffer(), C.LDim(), cs);
+        if (gpu) {
+            ELX_CHECK_HIP(hipEventRecord(s.done, cs));
+            s.pending = true;
+        }
+    };
+    if (np > 0) issue(0);
+    for (int p = 0; p < np; ++p) {
+        if (p + 1 < np) issue(p + 1);
+        compute(p);
+    }
+    if (gpu) {
+        // temporaries are freed on the comm stream: order that after the last update
+        FenceStreams(cs, ms);
+        for (auto& s : slot) {
+            s.ua.reset();
+            s.ub.reset();
+            s.a.reset();
+            s.b.reset();
+            ELX_CHECK_HIP(hipEventDestroy(s.ready));
+            ELX_CHECK_HIP(hipEventDestroy(s.done));
+        }
+    }
+    Cp.Finish();
+}
+
+// ---------------------------------------------------------------------------
+// A-stationary (keeps A, reduces partial C panels): NN.hpp:107-154, NT.hpp:19-59,
+// TN.hpp:19-61, TT.hpp:17-61.  Loop over column panels of C.
+// ---------------------------------------------------------------------------
+void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    RWProxy Cp(CPre);
+    const DistMatrix& A = *Ap;
+    const DistMatrix& B = *Bp;
+    DistMatrix& C = Cp.Get();
+    const Int n = C.Width(), nb = g_blocksize;
+    for (Int k = 0; k < n; k += nb) {
+        const Int k1 = std::min(n, k + nb);
+        auto C1 = DistMatrix::View(C, 0, C.Height(), k, k1);
+        if (IsN(oA)) {
+            // D1[MC,*] := alpha A[MC,MR] op(B)1[MR,*];  C1 += sum over MR
+            auto B1 = IsN(oB) ? DistMatrix::View(B, 0, B.Height(), k, k1) : DistMatrix::View(B, k, k1, 0, B.Width());
+            auto B1T = B.Like(Dist::STAR, Dist::MR);  // (op(B)1)^T with cols over MR
+            B1T->AlignWith(A, true);
+            if (IsN(oB)) Transpose(*B1, *B1T); else Copy(*B1, *B1T);
+            auto D1 = A.Like(Dist::MC, Dist::STAR);
+            D1->AlignWith(A, true);
+            LocalGemmResize(ELX_NORMAL, ELX_TRANSPOSE, alpha, A, *B1T, *D1);
+            AxpyContract(1.0, *D1, *C1);
+        } else {
+            // D1[MR,*] := alpha A^T[MR,MC] op(B)1[MC,*];  C1 += sum over MC, transposed dist
+            auto B1 = IsN(oB) ? DistMatrix::View(B, 0, B.Height(), k, k1) : DistMatrix::View(B, k, k1, 0, B.Width());
+            auto B1m = B.Like(Dist::MC, Dist::STAR);  // op(B)1 rows over MC
+            B1m->AlignWith(A, true);
+            if (IsN(oB)) Copy(*B1, *B1m); else Transpose(*B1, *B1m);
+            auto D1 = A.Like(Dist::MR, Dist::STAR);
+            D1->AlignWith(A, true);
+            LocalGemmResize(ELX_TRANSPOSE, ELX_NORMAL, alpha, A, *B1m, *D1);
+            AxpyContract(1.0, *D1, *C1);  // [MR,*] -> [MC,MR]: reduce over MC + exchange
+        }
+    }
+    Cp.Finish();
+}
+
+// ---------------------------------------------------------------------------
+// B-stationary (keeps B, reduces partial C row panels): NN.hpp:226-270,
+// NT.hpp:134-176, TN.hpp:137-176, TT.hpp:105-152.  Loop over row panels of C.
+// ---------------------------------------------------------------------------
+void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    RWProxy Cp(CPre);
+    const DistMatrix& A = *Ap;
+    const DistMatrix& B = *Bp;
+    DistMatrix& C = Cp.Get();
+    const Int m = C.Height(), nb = g_blocksize;
+    for (Int k = 0; k < m; k += nb) {
+        const Int k1 = std::min(m, k + nb);
+        auto C1 = DistMatrix::View(C, k, k1, 0, C.Width());
+        // op(A)1 = rows k..k1 of op(A)
+        auto A1 = IsN(oA) ? DistMatrix::View(A, k, k1, 0, A.Width()) : DistMatrix::View(A, 0, A.Height(), k, k1);
+        if (IsN(oB)) {
+            // D1^T[MR,*] := alpha B^T[MR,MC] (op(A)1)^T[MC,*]; C1 += transposed sum over MC
+            auto A1T = A.Like(Dist::STAR, Dist::MC);  // op(A)1 with cols over MC
+            A1T->AlignWith(B, true);
+            if (IsN(oA)) Copy(*A1, *A1T); else Transpose(*A1, *A1T);
+            auto D1T = B.Like(Dist::MR, Dist::STAR);
+            D1T->AlignWith(B, true);
+            LocalGemmResize(ELX_TRANSPOSE, ELX_TRANSPOSE, alpha, B, *A1T, *D1T);
+            TransposeAxpyContract(1.0, *D1T, *C1);
+        } else {
+            // D1[*,MC] := alpha op(A)1[*,MR] B^T[MR,MC]; C1 += sum over MR then redistribute
+            auto A1r = A.Like(Dist::STAR, Dist::MR);
+            A1r->AlignWith(B, true);
+            if (IsN(oA)) Copy(*A1, *A1r); else Transpose(*A1, *A1r);
+            auto D1 = B.Like(Dist::STAR, Dist::MC);
+            D1->AlignWith(B, true);
+            LocalGemmResize(ELX_NORMAL, ELX_TRANSPOSE, alpha, *A1r, B, *D1);
+            AxpyContract(1.0, *D1, *C1);
+        }
+    }
+    Cp.Finish();
+}
+
+// ---------------------------------------------------------------------------
+// Dot (1-D inner products over all p ranks): NN.hpp:461-511, NT.hpp:373-418,
+// TN.hpp:371-416 (config C4), TT.hpp:287-333.  op(A) -> k distributed VC,
+// 2000x2000 blocks of C summed with a reduce-scatter over all ranks.
+// ---------------------------------------------------------------------------
+void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
+              Int bs) {
+    const Int m = CPre.Height(), n = CPre.Width();
+    // k must be distributed VC on both: op(A) = A ([*,VC]) or A^T ([VC,*])
+    auto Ap = IsN(oA) ? ReadProxy(APre, Dist::STAR, Dist::VC) : ReadProxy(APre, Dist::VC, Dist::STAR);
+    const int kAlign = IsN(oA) ? Ap->RowAlign() : Ap->ColAlign();
+    auto Bp = IsN(oB) ? ReadProxy(BPre, Dist::VC, Dist::STAR, kAlign, -1) : ReadProxy(BPre, Dist::STAR, Dist::VC, -1, kAlign);
+    RWProxy Cp(CPre);
+    const DistMatrix& A = *Ap;
+    const DistMatrix& B = *Bp;
+    DistMatrix& C = Cp.Get();
+    auto C11 = C.Like(Dist::STAR, Dist::STAR);
+    for (Int i0 = 0; i0 < m; i0 += bs) {
+        const Int i1 = std::min(m, i0 + bs);
+        auto A1 = IsN(oA) ? DistMatrix::View(A, i0, i1, 0, A.Width()) : DistMatrix::View(A, 0, A.Height(), i0, i1);
+        for (Int j0 = 0; j0 < n; j0 += bs) {
+            const Int j1 = std::min(n, j0 + bs);
+            auto B1 = IsN(oB) ? DistMatrix::View(B, 0, B.Height(), j0, j1) : DistMatrix::View(B, j0, j1, 0, B.Width());
+            auto C1 = DistMatrix::View(C, i0, i1, j0, j1);
+            LocalGemmResize(oA, oB, alpha, *A1, *B1, *C11);
+            AxpyContract(1.0, *C11, *C1);
+        }
+    }
+    Cp.Finish();
+}
+
+int Heuristic(Int m, Int n, Int k) {  // NN.hpp:583-600 (same weights in NT/TN/TT)
+    const double wC = 2.0, wDot = 10.0;
+    if (wDot * m <= k && wDot * n <= k) return ELX_GEMM_SUMMA_DOT;
+    if (m <= n && wC * m <= k) return ELX_GEMM_SUMMA_B;
+    if (n <= m && wC * n <= k) return ELX_GEMM_SUMMA_A;
+    return ELX_GEMM_SUMMA_C;
+}
+
+}  // namespace
+
+void SetBlocksize(Int nb) { ELX_REQUIRE(nb > 0, "blocksize must be positive"); g_blocksize = nb; }
+Int Blocksize() { return g_blocksize; }
+void SetComputePanel(Int kc) { ELX_REQUIRE(kc >= 0, "compute panel must be >= 0"); g_compute_panel = kc; }
+Int ComputePanel() { return g_compute_panel; }
+int LastGemmAlgorithm() { return g_last_alg; }
+
+void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C) {
+    ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "LocalGemm: mixed types");
+    ELX_REQUIRE(A.Dev() == B.Dev() && A.Dev() == C.Dev(), "LocalGemm: mixed devices");
+    // the reference's conformance checks (src/blas_like/level3/Gemm.cpp:326-423)
+    const Dist aR = IsN(oA) ? A.ColDist() : A.RowDist(), aK = IsN(oA) ? A.RowDist() : A.ColDist();
+    const Dist bK = IsN(oB) ? B.ColDist() : B.RowDist(), bC = IsN(oB) ? B.RowDist() : B.ColDist();
+    const int aRa = IsN(oA) ? A.ColAlign() : A.RowAlign(), aKa = IsN(oA) ? A.RowAlign() : A.ColAlign();
+    const int bKa = IsN(oB) ? B.ColAlign() : B.RowAlign(), bCa = IsN(oB) ? B.RowAlign() : B.ColAlign();
+    const Int am = IsN(oA) ? A.Height() : A.Width(), ak = IsN(oA) ? A.Width() : A.Height();
+    const Int bk = IsN(oB) ? B.Height() : B.Width(), bn = IsN(oB) ? B.Width() : B.Height();
+    Check(aR == C.ColDist() && aK == bK && bC == C.RowDist(), "A, B and C do not have compatible distributions");
+    Check(aRa == C.ColAlign() && aKa == bKa && bCa == C.RowAlign(), "A, B and C are not aligned");
+    Check(am == C.Height() && ak == bk && bn == C.Width(), "nonconformal");
+    const Int m = C.LocalHeight(), n = C.LocalWidth();
+    const Int k = IsN(oA) ? A.LocalWidth() : A.LocalHeight();
+    if (m == 0 || n == 0) return;
+    if (k == 0) {  // Gemm.cpp:240-248
+        Scale(beta, C);
+        return;
+    }
+    if (C.Dev() == Device::GPU) {
+        FenceStreams(A.Stream(), C.Stream());
+        FenceStreams(B.Stream(), C.Stream());
+    }
+    exec::Gemm(C.Dev(), C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
+               beta, C.Buffer(), C.LDim(), C.Stream());
+}
+
+void LocalGemmResize(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, DistMatrix& C) {
+    const Int m = IsN(oA) ? A.Height() : A.Width();
+    const Int n = IsN(oB) ? B.Width() : B.Height();
+    const int ca = IsN(oA) ? A.ColAlign() : A.RowAlign();
+    const int ra = IsN(oB) ? B.RowAlign() : B.ColAlign();
+    if (!C.Viewing()) {
+        if (!C.ColConstrained() || C.ColAlign() != ca) C.AlignCols(ca % C.ColStride(), false);
+        if (!C.RowConstrained() || C.RowAlign() != ra) C.AlignRows(ra % C.RowStride(), false);
+    }
+    C.Resize(m, n);
+    LocalGemm(oA, oB, alpha, A, B, 0.0, C);
+}
+
+void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,
+          int alg) {
+    ELX_REQUIRE(oA >= ELX_NORMAL && oA <= ELX_ADJOINT && oB >= ELX_NORMAL && oB <= ELX_ADJOINT, "bad orientation");
+    ELX_REQUIRE(&A.G() == &B.G() && &A.G() == &C.G(), "Gemm: matrices on different grids");
+    ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "Gemm: mixed types");
+    // real types: ADJOINT == TRANSPOSE
+    if (oA == ELX_ADJOINT) oA = ELX_TRANSPOSE;
+    if (oB == ELX_ADJOINT) oB = ELX_TRANSPOSE;
+    const Int m = IsN(oA) ? A.Height() : A.Width(), k = IsN(oA) ? A.Width() : A.Height();
+    const Int kb = IsN(oB) ? B.Height() : B.Width(), n = IsN(oB) ? B.Width() : B.Height();
+    ELX_REQUIRE(m == C.Height() && n == C.Width() && k == kb, "Gemm: nonconformal ", m, "x", k, " * ", kb, "x", n,
+                " -> ", C.Height(), "x", C.Width());
+    Scale(beta, C);  // Gemm.cpp:282
+    if (alg == ELX_GEMM_DEFAULT) alg = Heuristic(m, n, k);
+    switch (alg) {
+    case ELX_GEMM_SUMMA_A_MS: case ELX_GEMM_SUMMA_A: SummaA(oA, oB, alpha, A, B, C); break;
+    case ELX_GEMM_SUMMA_B_MS: case ELX_GEMM_SUMMA_B: SummaB(oA, oB, alpha, A, B, C); break;
+    case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, C); break;
+    case ELX_GEMM_SUMMA_DOT: SummaDot(oA, oB, alpha, A, B, C, kDotBlock); break;
+    case ELX_GEMM_CANNON:
+        throw UnsupportedError("GEMM_CANNON: the reference runs Cannon on the CPU only (NN.hpp:30-31); "
+                               "not part of the MI355X path");
+    default: throw LogicError(Cat("Unsupported Gemm option ", alg));
+    }
+    g_last_alg = alg;
+}
+
+}  // namespace elx

@@ -1,0 +1,397 @@
+// The redistribution engine.
+//
+// The reference dispatches each (source, target) distribution pair to one of
+// ~20 hand-written routines (include/El/blas_like/level1/Copy/*.hpp:
+// RowAllGather, ColAllGather, PartialRow/ColAllGather, Col/RowAllToAllDemote/
+// Promote, Exchange, Filter, Scatter, Gather, TranslateBetweenGrids, ...),
+// each one pack -> MPI collective -> unpack, chained over up to three hops for
+// pairs without a direct routine (e.g. MC_MR.cpp:85-139).
+//
+// Here every pair goes through ONE plan, computed from the layout formulas:
+// for each peer pair (s -> d) the elements s sends to d are a Cartesian product
+// I(s,d) x J(s,d) of two residue classes (CRT on the two cyclic patterns), so
+// the pack and the unpack are single strided 2-D block moves.  Replicated
+// sources send from one designated owner (the one that shares the receiver's
+// free grid coordinates, i.e. the receiver itself whenever it already holds
+// the data), so each element crosses the network at most once per receiver -
+// the same bytes as the reference's AllGather/AllToAll/SendRecv chains, in one
+// hop.  Execution: one batched pack launch, one grouped RCCL send/recv over the
+// VC communicator (direct xGMI peer links), one batched unpack launch.  The
+// result is bit-exact by construction (pure data movement).
+#include "redist.hpp"
+#include "exec.hpp"
+#include <numeric>
+#include <vector>
+
+namespace elx {
+
+namespace {
+
+struct DimXfer {
+    Int count = 0;
+    Int src0 = 0, src_step = 1;  // first local index / step in the source
+    Int dst0 = 0, dst_step = 1;  // ... in the target
+};
+
+Int Gcd(Int a, Int b) { while (b) { Int t = a % b; a = b; b = t; } return a; }
+
+// Global indices in [0,n) held by source coordinate rs (stride ss, align as)
+// AND wanted by target coordinate rd (stride sd, align ad).
+DimXfer Intersect(Int n, int ss, int rs, int as, int sd, int rd, int ad) {
+    DimXfer x;
+    if (rs < 0 || rd < 0 || n == 0) return x;
+    const Int shs = Shift(rs, as, ss), shd = Shift(rd, ad, sd);
+    const Int L = ss / Gcd(ss, sd) * sd;
+    for (Int z = shs; z < L; z += ss) {
+        if (Mod(z - shd, sd) == 0) {
+            x.count = Length(n, z, L);
+            x.src0 = (z - shs) / ss;
+            x.src_step = L / ss;
+            x.dst0 = (z - shd) / sd;
+            x.dst_step = L / sd;
+            return x;
+        }
+    }
+    return x;
+}
+
+bool FixesMC(Dist d) { return d == Dist::MC || d == Dist::VC || d == Dist::VR; }
+bool FixesMR(Dist d) { return d == Dist::MR || d == Dist::VC || d == Dist::VR; }
+
+// Is source rank s the designated sender of A's data to receiver d?
+bool Designated(const DistMatrix& A, int s, int d) {
+    if (!A.ParticipatingOf(s)) return false;
+    if (A.ColDist() == Dist::CIRC) return true;
+    const Grid& g = A.G();
+    const bool fmc = FixesMC(A.ColDist()) || FixesMC(A.RowDist());
+    const bool fmr = FixesMR(A.ColDist()) || FixesMR(A.RowDist());
+    return (fmc || g.MCOf(s) == g.MCOf(d)) && (fmr || g.MROf(s) == g.MROf(d));
+}
+
+struct PairPlan {
+    DimXfer rows, cols;
+    Int count() const { return rows.count * cols.count; }
+};
+
+PairPlan Plan(const DistMatrix& A, const DistMatrix& B, int s, int d) {
+    PairPlan p;
+    p.rows = Intersect(A.Height(), A.ColStride(), A.ColRankOf(s), A.ColAlign(), B.ColStride(), B.ColRankOf(d),
+                       B.ColAlign());
+    p.cols = Intersect(A.Width(), A.RowStride(), A.RowRankOf(s), A.RowAlign(), B.RowStride(), B.RowRankOf(d),
+                       B.RowAlign());
+    if (p.rows.count == 0 || p.cols.count == 0) p.rows.count = p.cols.count = 0;
+    return p;
+}
+
+char* At(const DistMatrix& M, Int iLoc, Int jLoc) {
+    return static_cast<char*>(M.Buffer()) + (iLoc + jLoc * M.LDim()) * static_cast<Int>(M.ElemSize());
+}
+
+// Order B's stream after A's pending work (the reference's MultiSync fencing,
+// include/hydrogen/MultiSync.hpp:33-78).
+void Fence(const DistMatrix& A, const DistMatrix& B) {
+    if (A.Dev() != Device::GPU || B.Dev() != Device::GPU || A.Stream() == B.Stream()) return;
+    hipEvent_t ev;
+    ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ELX_CHECK_HIP(hipEventRecord(ev, A.Stream()));
+    ELX_CHECK_HIP(hipStreamWaitEvent(B.Stream(), ev, 0));
+    ELX_CHECK_HIP(hipEventDestroy(ev));
+}
+
+// Alignment an unconstrained target adopts from its source, per dimension,
+// following the one-hop copy routines: same dist -> same align
+// (Copy/Translate); target is the partial of the source (VC->MC) -> align mod
+// stride (ColAllToAllPromote.hpp:26, PartialColAllGather.hpp:43); source is the
+// partial of the target (MC->VC) -> same align (ColAllToAllDemote.hpp:25);
+// STAR -> 0; the source's other dimension of the same dist -> its align
+// (transposing pairs, AlignColsWith ElementMatrix.cpp:243-269); else unchanged.
+int AdoptAlign(Dist target, int stride, int cur, Dist srcSame, int alignSame, Dist srcOther, int alignOther) {
+    auto partial = [](Dist u) { return u == Dist::VC ? Dist::MC : (u == Dist::VR ? Dist::MR : u); };
+    if (target == Dist::STAR || target == Dist::CIRC) return 0;
+    if (srcSame == target) return alignSame % stride;
+    if (partial(srcSame) == target) return alignSame % stride;
+    if (partial(target) == srcSame) return alignSame % stride;
+    if (srcOther == target) return alignOther % stride;
+    return cur;
+}
+
+void PrepareTarget(const DistMatrix& A, DistMatrix& B) {
+    if (!B.Viewing()) {
+        if (!B.ColConstrained())
+            B.AlignCols(AdoptAlign(B.ColDist(), B.ColStride(), B.ColAlign(), A.ColDist(), A.ColAlign(), A.RowDist(),
+                                   A.RowAlign()), false);
+        if (!B.RowConstrained())
+            B.AlignRows(AdoptAlign(B.RowDist(), B.RowStride(), B.RowAlign(), A.RowDist(), A.RowAlign(), A.ColDist(),
+                                   A.ColAlign()), false);
+    }
+    B.Resize(A.Height(), A.Width());
+}
+
+void CheckCompatible(const DistMatrix& A, const DistMatrix& B) {
+    ELX_REQUIRE(A.Type() == B.Type(), "redistribution between different types (", DTypeName(A.Type()), " -> ",
+                DTypeName(B.Type()), ")");
+    ELX_REQUIRE(&A.G() == &B.G(), "matrices live on different grids");
+}
+
+// Cross-device copy of A's local data into an identically distributed matrix on `dev`.
+std::shared_ptr<DistMatrix> OnDevice(const DistMatrix& A, Device dev, hipStream_t s) {
+    auto T = std::make_shared<DistMatrix>(A.GridPtr(), A.Type(), A.ColDist(), A.RowDist(), dev, A.Root());
+    T->Align(A.ColAlign(), A.RowAlign(), true);
+    T->Resize(A.Height(), A.Width());
+    if (T->LocalHeight() > 0 && T->LocalWidth() > 0) {
+        const size_t es = A.ElemSize();
+        const hipMemcpyKind kind = dev == Device::GPU ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+        hipStream_t st = dev == Device::GPU ? T->Stream() : A.Stream();
+        if (dev == Device::CPU) A.Synchronize();
+        ELX_CHECK_HIP(hipMemcpy2DAsync(T->Buffer(), T->LDim() * es, A.Buffer(), A.LDim() * es,
+                                       A.LocalHeight() * es, A.LocalWidth(), kind, st));
+        ELX_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    (void)s;
+    return T;
+}
+
+// Shared transfer for Copy (designated senders, overwrite) and AxpyContract
+// (every owner sends, receiver sums in rank order).
+void Transfer(const DistMatrix& A, DistMatrix& B, bool contract, double alpha) {
+    const Grid& g = A.G();
+    const int p = g.Size(), me = g.VCRank();
+    const DType t = A.Type();
+    const Device dev = B.Dev();
+    const size_t es = A.ElemSize();
+    hipStream_t st = B.Stream();
+    Fence(A, B);
+
+    auto sends_to = [&](int s, int d) { return contract ? A.ParticipatingOf(s) : Designated(A, s, d); };
+
+    bool cross = false;  // does any rank exchange data with another? (same answer on every rank)
+    for (int s = 0; s < p && !cross; ++s)
+        for (int d = 0; d < p && !cross; ++d)
+            if (s != d && sends_to(s, d) && Plan(A, B, s, d).count() > 0) cross = true;
+
+    std::vector<PairPlan> out(p), in(p);
+    std::vector<Int> sc(p, 0), sd(p, 0), rc(p, 0), rd(p, 0);
+    Int stot = 0, rtot = 0;
+    for (int q = 0; q < p; ++q) {
+        if (sends_to(me, q)) out[q] = Plan(A, B, me, q);
+        if (sends_to(q, me)) in[q] = Plan(A, B, q, me);
+        if (q == me) continue;
+        sc[q] = out[q].count(); sd[q] = stot; stot += sc[q];
+        rc[q] = in[q].count();  rd[q] = rtot; rtot += rc[q];
+    }
+
+    // the local portion moves directly (never through the send buffer)
+    auto local_desc = [&](const PairPlan& pl) {
+        return kern::Copy2D{pl.rows.count, pl.cols.count,
+                            At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step, pl.cols.src_step * A.LDim(),
+                            At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step, pl.cols.dst_step * B.LDim()};
+    };
+
+    elx::Buffer sbuf, rbuf;
+    if (cross) {
+        sbuf.Reset(dev, static_cast<size_t>(stot) * es, st);
+        rbuf.Reset(dev, static_cast<size_t>(rtot) * es, st);
+        std::vector<kern::Copy2D> pack;
+        for (int q = 0; q < p; ++q) {
+            if (q == me || sc[q] == 0) continue;
+            const PairPlan& pl = out[q];
+            pack.push_back({pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
+                            pl.cols.src_step * A.LDim(), static_cast<char*>(sbuf.data()) + sd[q] * es, 1,
+                            pl.rows.count});
+        }
+        exec::Copy2DBatch(dev, t, pack.data(), static_cast<int>(pack.size()), false, 0.0, st);
+    }
+    if (!contract && out[me].count() > 0) {
+        auto d = local_desc(out[me]);
+        exec::Copy2DBatch(dev, t, &d, 1, false, 0.0, st);
+    }
+    if (cross) g.VC().AllToAllV(t, sbuf.data(), sc, sd, rbuf.data(), rc, rd, dev, st);
+
+    auto unpack_desc = [&](int q) {
+        const PairPlan& pl = in[q];
+        return kern::Copy2D{pl.rows.count, pl.cols.count, static_cast<char*>(rbuf.data()) + rd[q] * es, 1,
+                            pl.rows.count, At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
+                            pl.cols.dst_step * B.LDim()};
+    };
+    if (!contract) {
+        std::vector<kern::Copy2D> unpack;
+        for (int q = 0; q < p; ++q)
+            if (q != me && rc[q] > 0) unpack.push_back(unpack_desc(q));
+        exec::Copy2DBatch(dev, t, unpack.data(), static_cast<int>(unpack.size()), false, 0.0, st);
+    } else {
+        // sum contributions in rank order (deterministic); one launch per source
+        // so two sources never update the same element concurrently
+        for (int q = 0; q < p; ++q) {
+            if (q == me) {
+                if (in[me].count() > 0) {
+                    auto d = local_desc(in[me]);
+                    exec::Copy2DBatch(dev, t, &d, 1, true, alpha, st);
+                }
+            } else if (rc[q] > 0) {
+                auto d = unpack_desc(q);
+                exec::Copy2DBatch(dev, t, &d, 1, true, alpha, st);
+            }
+        }
+    }
+    // sbuf/rbuf return to the pool stream-ordered on `st`
+}
+
+void LocalTransposeInto(const DistMatrix& A, DistMatrix& T) {
+    // T's local block is A's local block transposed
+    if (T.LocalHeight() == 0 || T.LocalWidth() == 0) return;
+    kern::Copy2D d{T.LocalHeight(), T.LocalWidth(), A.Buffer(), A.LDim(), 1, T.Buffer(), 1, T.LDim()};
+    Fence(A, T);
+    exec::Copy2DBatch(T.Dev(), T.Type(), &d, 1, false, 0.0, T.Stream());
+}
+
+std::shared_ptr<DistMatrix> LocalTransposed(const DistMatrix& A) {
+    auto T = A.Like(A.RowDist(), A.ColDist());
+    T->Align(A.RowAlign(), A.ColAlign(), true);
+    T->Resize(A.Width(), A.Height());
+    LocalTransposeInto(A, *T);
+    return T;
+}
+
+}  // namespace
+
+bool SameLocalLayout(const DistMatrix& A, Dist cd, Dist rd, int calign, int ralign) {
+    const Grid& g = A.G();
+    if (A.ColDist() == Dist::CIRC || cd == Dist::CIRC) return false;
+    if (g.Stride(cd) != A.ColStride() || g.Stride(rd) != A.RowStride()) return false;
+    for (int q = 0; q < g.Size(); ++q) {
+        if (Shift(g.DistRankOf(cd, q), calign, g.Stride(cd)) != Shift(A.ColRankOf(q), A.ColAlign(), A.ColStride()))
+            return false;
+        if (Shift(g.DistRankOf(rd, q), ralign, g.Stride(rd)) != Shift(A.RowRankOf(q), A.RowAlign(), A.RowStride()))
+            return false;
+    }
+    return true;
+}
+
+void Copy(const DistMatrix& A, DistMatrix& B) {
+    CheckCompatible(A, B);
+    if (A.Dev() != B.Dev()) {
+        auto T = OnDevice(A, B.Dev(), B.Stream());
+        Copy(*T, B);
+        return;
+    }
+    PrepareTarget(A, B);
+    if (B.Height() == 0 || B.Width() == 0) return;
+    Transfer(A, B, false, 0.0);
+}
+
+void Transpose(const DistMatrix& A, DistMatrix& B) {
+    CheckCompatible(A, B);
+    if (A.Dev() == B.Dev() && B.ColDist() == A.RowDist() && B.RowDist() == A.ColDist()) {
+        // direct local transpose when B can hold A^T with matching alignment
+        const bool colOk = B.Viewing() || B.ColConstrained() ? B.ColAlign() == A.RowAlign() : true;
+        const bool rowOk = B.Viewing() || B.RowConstrained() ? B.RowAlign() == A.ColAlign() : true;
+        if (colOk && rowOk) {
+            if (!B.Viewing()) {
+                if (!B.ColConstrained()) B.AlignCols(A.RowAlign(), false);
+                if (!B.RowConstrained()) B.AlignRows(A.ColAlign(), false);
+            }
+            B.Resize(A.Width(), A.Height());
+            LocalTransposeInto(A, B);
+            return;
+        }
+    }
+    auto T = LocalTransposed(A);
+    Copy(*T, B);
+}
+
+void AxpyContract(double alpha, const DistMatrix& A, DistMatrix& B) {
+    CheckCompatible(A, B);
+    ELX_REQUIRE(A.Height() == B.Height() && A.Width() == B.Width(), "AxpyContract: ", A.Height(), "x", A.Width(),
+                " vs ", B.Height(), "x", B.Width());
+    if (A.Dev() != B.Dev()) {
+        auto T = OnDevice(A, B.Dev(), B.Stream());
+        AxpyContract(alpha, *T, B);
+        return;
+    }
+    if (B.Height() == 0 || B.Width() == 0) return;
+    Transfer(A, B, true, alpha);
+}
+
+void TransposeAxpyContract(double alpha, const DistMatrix& A, DistMatrix& B) {
+    auto T = LocalTransposed(A);
+    AxpyContract(alpha, *T, B);
+}
+
+void Axpy(double alpha, const DistMatrix& X, DistMatrix& Y) {
+    CheckCompatible(X, Y);
+    ELX_REQUIRE(X.Height() == Y.Height() && X.Width() == Y.Width(), "Axpy: nonconformal ", X.Height(), "x",
+                X.Width(), " vs ", Y.Height(), "x", Y.Width());
+    if (X.Dev() == Y.Dev() && X.ColDist() == Y.ColDist() && X.RowDist() == Y.RowDist() &&
+        X.ColAlign() == Y.ColAlign() && X.RowAlign() == Y.RowAlign()) {
+        if (Y.LocalHeight() == 0 || Y.LocalWidth() == 0) return;
+        kern::Copy2D d{Y.LocalHeight(), Y.LocalWidth(), X.Buffer(), 1, X.LDim(), Y.Buffer(), 1, Y.LDim()};
+        Fence(X, Y);
+        exec::Copy2DBatch(Y.Dev(), Y.Type(), &d, 1, true, alpha, Y.Stream());
+        return;
+    }
+    auto T = Y.Like(Y.ColDist(), Y.RowDist());
+    T->Align(Y.ColAlign(), Y.RowAlign(), true);
+    Copy(X, *T);
+    Axpy(alpha, *T, Y);
+}
+
+void Zero(DistMatrix& A) {
+    if (A.LocalHeight() == 0 || A.LocalWidth() == 0) return;
+    exec::Fill(A.Dev(), A.Type(), A.LocalHeight(), A.LocalWidth(), 0.0, A.Buffer(), A.LDim(), A.Stream());
+}
+
+void Scale(double alpha, DistMatrix& A) {  // include/El/blas_like/level1/Scale.hpp:18-31
+    if (alpha == 0.0) { Zero(A); return; }
+    if (alpha == 1.0) return;
+    if (A.LocalHeight() == 0 || A.LocalWidth() == 0) return;
+    exec::Scale(A.Dev(), A.Type(), A.LocalHeight(), A.LocalWidth(), alpha, A.Buffer(), A.LDim(), A.Stream());
+}
+
+void Hadamard(const DistMatrix& A, const DistMatrix& B, DistMatrix& C) {  // Hadamard.hpp:107-131
+    CheckCompatible(A, B);
+    CheckCompatible(A, C);
+    ELX_REQUIRE(A.ColDist() == B.ColDist() && A.RowDist() == B.RowDist() && A.ColDist() == C.ColDist() &&
+                    A.RowDist() == C.RowDist(), "Hadamard: A, B and C must share a distribution");
+    ELX_REQUIRE(A.ColAlign() == B.ColAlign() && A.RowAlign() == B.RowAlign(), "Hadamard: A and B not aligned");
+    ELX_REQUIRE(A.Height() == B.Height() && A.Width() == B.Width(), "Hadamard: nonconformal");
+    ELX_REQUIRE(A.Dev() == B.Dev() && A.Dev() == C.Dev(), "Hadamard: mixed devices");
+    if (&C != &A && &C != &B) {
+        if (!C.Viewing()) {
+            if (!C.ColConstrained()) C.AlignCols(A.ColAlign(), false);
+            if (!C.RowConstrained()) C.AlignRows(A.RowAlign(), false);
+        }
+        ELX_REQUIRE(C.ColAlign() == A.ColAlign() && C.RowAlign() == A.RowAlign(), "Hadamard: C not aligned");
+        C.Resize(A.Height(), A.Width());
+    }
+    if (C.LocalHeight() == 0 || C.LocalWidth() == 0) return;
+    Fence(A, C);
+    Fence(B, C);
+    exec::Hadamard(C.Dev(), C.Type(), C.LocalHeight(), C.LocalWidth(), A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
+                   C.Buffer(), C.LDim(), C.Stream());
+}
+
+void EntrywiseMap(int fn, const DistMatrix& A, DistMatrix& B) {  // EntrywiseMap.hpp:90-137
+    CheckCompatible(A, B);
+    const DistMatrix* src = &A;
+    std::shared_ptr<DistMatrix> T;
+    if (A.ColDist() == B.ColDist() && A.RowDist() == B.RowDist() && A.Dev() == B.Dev()) {
+        if (!B.Viewing()) {
+            if (!B.ColConstrained()) B.AlignCols(A.ColAlign(), false);
+            if (!B.RowConstrained()) B.AlignRows(A.RowAlign(), false);
+        }
+    }
+    if (!(A.ColDist() == B.ColDist() && A.RowDist() == B.RowDist() && A.ColAlign() == B.ColAlign() &&
+          A.RowAlign() == B.RowAlign() && A.Dev() == B.Dev())) {
+        T = B.Like(B.ColDist(), B.RowDist());
+        T->Align(B.ColAlign(), B.RowAlign(), true);
+        Copy(A, *T);
+        src = T.get();
+    }
+    B.Resize(A.Height(), A.Width());
+    if (B.LocalHeight() == 0 || B.LocalWidth() == 0) return;
+    Fence(*src, B);
+    exec::Map(B.Dev(), B.Type(), fn, B.LocalHeight(), B.LocalWidth(), src->Buffer(), src->LDim(), B.Buffer(),
+              B.LDim(), B.Stream());
+}
+
+}  // namespace elx

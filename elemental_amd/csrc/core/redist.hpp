@@ -1,0 +1,26 @@
+// The DistMatrix redistribution engine and the distributed BLAS-1 front doors.
+#pragma once
+#include "distmatrix.hpp"
+
+namespace elx {
+
+// B := A (DistMatrix::operator=), any element-wise pair, any alignments.
+void Copy(const DistMatrix& A, DistMatrix& B);
+// B := A^T (El::Transpose on DistMatrices; ADJOINT == TRANSPOSE for real types)
+void Transpose(const DistMatrix& A, DistMatrix& B);
+// B += alpha * (sum of A's redundant partial copies), redistributed to B (AxpyContract)
+void AxpyContract(double alpha, const DistMatrix& A, DistMatrix& B);
+// same, but B's data first comes from A^T (TransposeAxpyContract)
+void TransposeAxpyContract(double alpha, const DistMatrix& A, DistMatrix& B);
+
+void Axpy(double alpha, const DistMatrix& X, DistMatrix& Y);
+void Scale(double alpha, DistMatrix& A);
+void Zero(DistMatrix& A);
+void Hadamard(const DistMatrix& A, const DistMatrix& B, DistMatrix& C);
+void EntrywiseMap(int fn, const DistMatrix& A, DistMatrix& B);
+
+// true iff A's local block already is B-with-B's-alignment's local block
+// (same owner of every element): lets SUMMA use views instead of copies.
+bool SameLocalLayout(const DistMatrix& A, Dist cd, Dist rd, int calign, int ralign);
+
+}  // namespace elx

@@ -1,0 +1,41 @@
+// Host-side launch interface of the gfx950 kernels (no exceptions; return hipError_t).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace elx {
+namespace kern {
+
+using i64 = int64_t;
+
+template <typename T>
+hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
+                     const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s);
+// 16-bit GEMMs: is_bf16 selects bf16 vs f16 storage; f32 accumulation.
+hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
+                       const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
+                       uint16_t* C, i64 ldc, hipStream_t s);
+
+// One strided 2-D block move: dst(i,j) (=|+=) alpha*src(i,j),
+// src(i,j) = src[i*scs + j*srs], dst(i,j) = dst[i*dcs + j*drs].
+struct Copy2D {
+    i64 m, n;
+    const void* src; i64 scs, srs;
+    void* dst; i64 dcs, drs;
+};
+constexpr int kMaxCopyBatch = 16;
+// Executes up to any number of descriptors (chunks of kMaxCopyBatch per launch).
+// axpy=false: plain copy (bit-exact, alpha ignored); axpy=true: dst += alpha*src.
+hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
+
+hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s);
+hipError_t scale2d(int dtype, i64 m, i64 n, double alpha, void* A, i64 lda, hipStream_t s);
+hipError_t hadamard2d(int dtype, i64 m, i64 n, const void* A, i64 lda, const void* B, i64 ldb,
+                      void* C, i64 ldc, hipStream_t s);
+hipError_t entrywise_map(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb,
+                         hipStream_t s);
+hipError_t fill_hash(int dtype, i64 m, i64 n, void* A, i64 lda, i64 i0, i64 istride, i64 j0,
+                     i64 jstride, uint64_t seed, double center, double radius, hipStream_t s);
+
+}  // namespace kern
+}  // namespace elx

@@ -1,0 +1,295 @@
+"""Thin Python mirror of the El:: objects on the GEMM path, over the C-ABI.
+
+Names and argument meaning follow the reference's C++ API (El::Grid,
+El::DistMatrix<T,U,V,ELEMENT,D>, El::Gemm, El::Axpy, ...), so parity tests
+read like the reference's own tests (tests/blas_like/Gemm.cpp,
+tests/core/DistMatrix.cpp).  All work happens in libelemental_amd.so; this
+module only moves handles and host arrays.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_double, c_int, c_int64, c_size_t, c_ubyte, c_void_p
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_CANNON, GEMM_DEFAULT,
+                   GEMM_SUMMA_A, GEMM_SUMMA_A_MS, GEMM_SUMMA_B, GEMM_SUMMA_B_MS, GEMM_SUMMA_C,
+                   GEMM_SUMMA_C_MS, GEMM_SUMMA_DOT, GPU, MC, MD, MR, NORMAL, ROW_MAJOR, STAR, TRANSPOSE,
+                   VC, VR, call, lib)
+
+__all__ = [
+    "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
+    "EntrywiseMap", "AxpyContract", "Transpose", "SetBlocksize", "Blocksize", "SetComputePanel",
+    "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
+    "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
+    "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
+    "ROW_MAJOR", "COLUMN_MAJOR", "DIST_NAMES", "VALID_DISTS", "np_dtype",
+]
+
+DIST_NAMES = {MC: "MC", MD: "MD", MR: "MR", VC: "VC", VR: "VR", STAR: "STAR", CIRC: "CIRC"}
+# every element-wise distribution on the GEMM path (MD pairs are out of scope)
+VALID_DISTS = [(MC, MR), (MC, STAR), (MR, MC), (MR, STAR), (STAR, MC), (STAR, MR), (STAR, STAR),
+               (STAR, VC), (STAR, VR), (VC, STAR), (VR, STAR), (CIRC, CIRC)]
+
+
+def np_dtype(t: int):
+    """Host storage dtype (bf16 travels as uint16 bit patterns)."""
+    return {F32: np.float32, F64: np.float64, F16: np.float16, BF16: np.uint16}[t]
+
+
+# --------------------------------------------------------------------- comm
+class Comm:
+    """World communicator: RCCL (device buffers), host bridge, or self."""
+
+    def __init__(self, handle, keepalive=None):
+        self.h = handle
+        self._keep = keepalive
+
+    @classmethod
+    def self_comm(cls) -> "Comm":
+        h = c_void_p()
+        call("elx_comm_init_host", byref(h), 0, 1, L.HOST_COLL_FN(), L.HOST_SPLIT_FN(), None)
+        return cls(h)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (c_ubyte * 128)()
+        call("elx_comm_unique_id", buf)
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, rank: int, size: int, uid: bytes) -> "Comm":
+        h = c_void_p()
+        buf = (c_ubyte * 128).from_buffer_copy(uid)
+        call("elx_comm_init_rccl", byref(h), rank, size, buf)
+        return cls(h)
+
+    @classmethod
+    def host(cls, bridge) -> "Comm":
+        """`bridge` implements the collectives (see torch_bridge.GlooBridge)."""
+        h = c_void_p()
+        call("elx_comm_init_host", byref(h), bridge.rank, bridge.size, bridge.coll_fn, bridge.split_fn, None)
+        return cls(h, keepalive=bridge)
+
+    @property
+    def rank(self) -> int:
+        r = c_int()
+        call("elx_comm_rank", self.h, byref(r))
+        return r.value
+
+    @property
+    def size(self) -> int:
+        s = c_int()
+        call("elx_comm_size", self.h, byref(s))
+        return s.value
+
+    def barrier(self):
+        call("elx_comm_barrier", self.h)
+
+
+# --------------------------------------------------------------------- grid
+class Grid:
+    """El::Grid(comm, height, order); height 0 -> Grid::DefaultHeight."""
+
+    def __init__(self, comm: Comm | None = None, height: int = 0, order: int = COLUMN_MAJOR):
+        self.comm = comm or Comm.self_comm()
+        h = c_void_p()
+        call("elx_grid_create", byref(h), self.comm.h, height, order)
+        self.h = h
+        info = (c_int * 8)()
+        call("elx_grid_info", self.h, info)
+        (self.height, self.width, self.size, self.rank, self.mc_rank, self.mr_rank, self.vc_rank,
+         self.vr_rank) = list(info)
+
+    @staticmethod
+    def default_height(size: int) -> int:
+        return lib().elx_grid_default_height(size)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().elx_grid_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+# --------------------------------------------------------------- distmatrix
+class DistMatrix:
+    """El::DistMatrix<T,U,V,ELEMENT,D>(grid, root)."""
+
+    def __init__(self, grid: Grid, dtype: int = F64, U: int = MC, V: int = MR, device: int = GPU,
+                 root: int = 0, height: int = 0, width: int = 0, _handle=None, _parent=None):
+        self.grid, self.dtype, self.U, self.V, self.device, self.root = grid, dtype, U, V, device, root
+        self._parent = _parent  # keep the viewed matrix alive
+        if _handle is None:
+            h = c_void_p()
+            call("elx_dm_create", byref(h), grid.h, dtype, U, V, device, root)
+            self.h = h
+            if height or width:
+                self.Resize(height, width)
+        else:
+            self.h = _handle
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().elx_dm_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # -- metadata
+    def info(self) -> dict:
+        v = (c_int64 * 13)()
+        call("elx_dm_info", self.h, v)
+        keys = ["height", "width", "local_height", "local_width", "ldim", "col_align", "row_align",
+                "col_shift", "row_shift", "col_stride", "row_stride", "participating", "viewing"]
+        return dict(zip(keys, list(v)))
+
+    def Height(self): return self.info()["height"]
+    def Width(self): return self.info()["width"]
+    def LocalHeight(self): return self.info()["local_height"]
+    def LocalWidth(self): return self.info()["local_width"]
+    def ColAlign(self): return self.info()["col_align"]
+    def RowAlign(self): return self.info()["row_align"]
+    def ColShift(self): return self.info()["col_shift"]
+    def RowShift(self): return self.info()["row_shift"]
+    def LDim(self): return self.info()["ldim"]
+
+    def Buffer(self) -> int:
+        p = c_void_p()
+        call("elx_dm_buffer", self.h, byref(p))
+        return p.value or 0
+
+    # -- shape / alignment
+    def Align(self, col_align: int, row_align: int, constrain: bool = True):
+        call("elx_dm_align", self.h, col_align, row_align, int(constrain))
+        return self
+
+    def AlignWith(self, other: "DistMatrix", constrain: bool = True):
+        call("elx_dm_align_with", self.h, other.h, int(constrain))
+        return self
+
+    def Resize(self, height: int, width: int):
+        call("elx_dm_resize", self.h, height, width)
+        return self
+
+    # -- data
+    def set_local(self, arr: np.ndarray):
+        arr = np.asfortranarray(arr, dtype=np_dtype(self.dtype))
+        i = self.info()
+        assert arr.shape == (i["local_height"], i["local_width"]), (arr.shape, i)
+        call("elx_dm_set_local", self.h, arr.ctypes.data_as(c_void_p), max(arr.shape[0], 1))
+
+    def get_local(self) -> np.ndarray:
+        i = self.info()
+        out = np.zeros((i["local_height"], i["local_width"]), dtype=np_dtype(self.dtype), order="F")
+        call("elx_dm_get_local", self.h, out.ctypes.data_as(c_void_p), max(out.shape[0], 1))
+        return out
+
+    def fill_hash(self, seed: int, center: float = 0.0, radius: float = 1.0):
+        """Grid-independent synthetic fill: A(i,j) = center + radius*u(seed,i,j)."""
+        call("elx_dm_fill_hash", self.h, seed, center, radius)
+        return self
+
+    def synchronize(self):
+        call("elx_dm_synchronize", self.h)
+
+    def __call__(self, rows, cols) -> "DistMatrix":
+        """A(IR(i0,i1), IR(j0,j1)) view; rows/cols are (start, stop) or slice(None)."""
+        i = self.info()
+        r0, r1 = (0, i["height"]) if rows is None or rows == slice(None) else rows
+        c0, c1 = (0, i["width"]) if cols is None or cols == slice(None) else cols
+        h = c_void_p()
+        call("elx_dm_view", byref(h), self.h, r0, r1, c0, c1)
+        return DistMatrix(self.grid, self.dtype, self.U, self.V, self.device, self.root, _handle=h, _parent=self)
+
+    def assign(self, other: "DistMatrix") -> "DistMatrix":
+        """self = other  (DistMatrix::operator=, any distribution pair)."""
+        call("elx_dm_copy", self.h, other.h)
+        return self
+
+    def like(self, U=None, V=None, device=None) -> "DistMatrix":
+        return DistMatrix(self.grid, self.dtype, self.U if U is None else U, self.V if V is None else V,
+                          self.device if device is None else device, self.root)
+
+
+# ------------------------------------------------------------ front doors
+def Gemm(orientA, orientB, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix,
+         alg: int = GEMM_DEFAULT) -> int:
+    """El::Gemm(orientA, orientB, alpha, A, B, beta, C, alg); returns the algorithm run."""
+    call("elx_gemm", orientA, orientB, float(alpha), A.h, B.h, float(beta), C.h, alg)
+    return lib().elx_last_gemm_algorithm()
+
+
+def LocalGemm(orientA, orientB, alpha, A, B, beta, C):
+    call("elx_local_gemm", orientA, orientB, float(alpha), A.h, B.h, float(beta), C.h)
+
+
+def Axpy(alpha, X: DistMatrix, Y: DistMatrix):
+    call("elx_dm_axpy", float(alpha), X.h, Y.h)
+
+
+def Scale(alpha, A: DistMatrix):
+    call("elx_dm_scale", float(alpha), A.h)
+
+
+def Zero(A: DistMatrix):
+    call("elx_dm_zero", A.h)
+
+
+def Hadamard(A, B, C):
+    call("elx_dm_hadamard", A.h, B.h, C.h)
+
+
+def EntrywiseMap(fn: int, A, B):
+    call("elx_dm_entrywise_map", fn, A.h, B.h)
+
+
+def AxpyContract(alpha, A, B):
+    call("elx_dm_axpy_contract", float(alpha), A.h, B.h)
+
+
+def Transpose(A, B):
+    call("elx_dm_transpose", A.h, B.h)
+
+
+def SetBlocksize(nb: int):
+    call("elx_set_blocksize", nb)
+
+
+def Blocksize() -> int:
+    return lib().elx_blocksize()
+
+
+def SetComputePanel(kc: int):
+    call("elx_set_compute_panel", kc)
+
+
+def comm_stats() -> dict:
+    b, s, c = c_int64(), c_double(), c_int64()
+    call("elx_comm_stats", byref(b), byref(s), byref(c))
+    return {"bytes": b.value, "seconds": s.value, "calls": c.value}
+
+
+def comm_stats_reset():
+    call("elx_comm_stats_reset")
+
+
+def device_count() -> int:
+    n = c_int()
+    call("elx_device_count", byref(n))
+    return n.value
+
+
+def device_synchronize():
+    call("elx_device_synchronize")
+
+
+def pool_stats() -> tuple[int, int]:
+    r, u = c_size_t(), c_size_t()
+    call("elx_pool_stats", byref(r), byref(u))
+    return r.value, u.value

@@ -1,0 +1,255 @@
+/*
+ * elemental_amd.h — C-ABI boundary of the MI355X-native El::Gemm path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers / sizes / enums,
+ * never throws, returns 0 on success and a nonzero ELX_ERR_* code on failure
+ * (message via elx_last_error()).  Device work is stream-ordered on the
+ * hipStream_t passed as `void* stream` (NULL = the library's compute stream).
+ * Callers keep ownership of every buffer they pass in.
+ *
+ * Each group below names the reference interface it replaces
+ * (paths relative to the reference tree, aj-prime/Elemental = LLNL Hydrogen).
+ */
+#ifndef ELEMENTAL_AMD_H
+#define ELEMENTAL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (mapped back to the reference's exception types) ------ */
+#define ELX_OK                  0
+#define ELX_ERR_LOGIC           1  /* El::LogicError  (std::logic_error)        */
+#define ELX_ERR_HIP             2  /* hydrogen::HIPError (H_CHECK_HIP)           */
+#define ELX_ERR_COMM            3  /* El::mpi error / Aluminum error             */
+#define ELX_ERR_RUNTIME         4  /* El::RuntimeError                           */
+#define ELX_ERR_UNSUPPORTED     5  /* "Bad device/type combo" LogicErrors        */
+#define ELX_ERR_NO_DEVICE       6  /* no gfx950 device visible                   */
+
+/* ---- enums: ordinals match the reference ------------------------------- */
+/* El::Orientation  include/El/core/types.hpp:463-469 */
+#define ELX_NORMAL     0
+#define ELX_TRANSPOSE  1
+#define ELX_ADJOINT    2
+/* El::Dist  include/El/core/types.hpp:207-217 */
+#define ELX_MC    0
+#define ELX_MD    1
+#define ELX_MR    2
+#define ELX_VC    3
+#define ELX_VR    4
+#define ELX_STAR  5
+#define ELX_CIRC  6
+/* El::GemmAlgorithm  include/El/blas_like/level3.hpp:22-35 */
+#define ELX_GEMM_DEFAULT    0
+#define ELX_GEMM_SUMMA_A_MS 1
+#define ELX_GEMM_SUMMA_A    2
+#define ELX_GEMM_SUMMA_B_MS 3
+#define ELX_GEMM_SUMMA_B    4
+#define ELX_GEMM_SUMMA_C_MS 5
+#define ELX_GEMM_SUMMA_C    6
+#define ELX_GEMM_SUMMA_DOT  7
+#define ELX_GEMM_CANNON     8
+/* El::GridOrder  include/El/core/types.hpp:408-413 */
+#define ELX_ROW_MAJOR    0
+#define ELX_COLUMN_MAJOR 1
+/* El::Device  include/hydrogen/Device.hpp */
+#define ELX_DEVICE_CPU 0
+#define ELX_DEVICE_GPU 1
+/* element types (the reference's GPU compute types + bf16, which it lacks) */
+#define ELX_F32  0
+#define ELX_F64  1
+#define ELX_F16  2   /* gpu_half_type (rocblas_half), include/hydrogen/utils/HalfPrecision.hpp:123 */
+#define ELX_BF16 3   /* new: no reference counterpart */
+/* entrywise functors for elx_entrywise_map (the C-ABI cannot carry a device
+ * lambda; the C++ header El/EntrywiseMap.hpp keeps the templated form)      */
+#define ELX_MAP_IDENTITY 0
+#define ELX_MAP_NEGATE   1
+#define ELX_MAP_ABS      2
+#define ELX_MAP_SQUARE   3
+#define ELX_MAP_SQRT     4
+#define ELX_MAP_EXP      5
+#define ELX_MAP_LOG      6
+#define ELX_MAP_RELU     7
+#define ELX_MAP_SIGMOID  8
+#define ELX_MAP_RECIP    9
+#define ELX_MAP_TANH     10
+
+/* ---- errors / runtime --------------------------------------------------- */
+/* replaces hydrogen::HIPError / H_CHECK_HIP (include/hydrogen/device/gpu/rocm/ROCmError.hpp) */
+const char* elx_last_error(void);
+int elx_version(void);
+/* replaces hydrogen::gpu::Initialize / ComputeDeviceId (src/hydrogen/device/GPU.cpp:30-67) */
+int elx_device_count(int* count);
+int elx_set_device(int device);
+int elx_get_device(int* device);
+int elx_device_synchronize(void);
+/* replaces SyncInfo<Device::GPU> {stream, event} (include/hydrogen/device/gpu/rocm/SyncInfo.hpp:15-41) */
+int elx_default_stream(void** stream);
+int elx_stream_create(void** stream);
+int elx_stream_destroy(void* stream);
+int elx_stream_synchronize(void* stream);
+
+/* ---- device memory pool: replaces the hipCUB CachingDeviceAllocator -----
+ * (src/core/imports/cub.cpp:1-75, El::Memory mode 1 include/El/core/Memory/impl.hpp:113-187) */
+int elx_pool_alloc(void** ptr, size_t bytes, void* stream);
+int elx_pool_free(void* ptr, void* stream);
+int elx_pool_trim(size_t bytes_to_keep);
+int elx_pool_stats(size_t* bytes_reserved, size_t* bytes_in_use);
+int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int elx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int elx_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+
+/* ---- local GEMM: replaces hydrogen::gpu_blas::Gemm -> rocblas_{h,s,d}gemm
+ * (include/hydrogen/blas/GPU_BLAS_impl.hpp:397-423, src/hydrogen/device/rocBLAS_API.cpp:151-170).
+ * Column-major C(m x n) := alpha op(A) op(B) + beta C; beta == 0 never reads C.
+ * f16/bf16 take/return 16-bit storage, accumulate in f32. */
+int elx_gemm_f64(int opA, int opB, int64_t m, int64_t n, int64_t k,
+                 double alpha, const double* A, int64_t lda,
+                 const double* B, int64_t ldb,
+                 double beta, double* C, int64_t ldc, void* stream);
+int elx_gemm_f32(int opA, int opB, int64_t m, int64_t n, int64_t k,
+                 float alpha, const float* A, int64_t lda,
+                 const float* B, int64_t ldb,
+                 float beta, float* C, int64_t ldc, void* stream);
+int elx_gemm_f16(int opA, int opB, int64_t m, int64_t n, int64_t k,
+                 float alpha, const uint16_t* A, int64_t lda,
+                 const uint16_t* B, int64_t ldb,
+                 float beta, uint16_t* C, int64_t ldc, void* stream);
+int elx_gemm_bf16(int opA, int opB, int64_t m, int64_t n, int64_t k,
+                  float alpha, const uint16_t* A, int64_t lda,
+                  const uint16_t* B, int64_t ldb,
+                  float beta, uint16_t* C, int64_t ldc, void* stream);
+
+/* ---- BLAS-1 entrywise kernels (dtype-generic; scalars passed as double) --
+ * Strides are element strides: X(i,j) = X[i*xcs + j*xrs].
+ * axpy2d   replaces Axpy_GPU_impl            (src/hydrogen/blas/gpu/Axpy.cu:119-189)
+ * copy2d   replaces Copy_GPU_impl            (src/hydrogen/blas/gpu/Copy.cu:104-205)
+ * transpose replaces Transpose_GPU_impl      (src/hydrogen/blas/gpu/Transpose.cu:102-127)
+ * scale2d  replaces Scale_GPU_impl           (src/hydrogen/blas/gpu/Scale.cu:45-81)
+ * fill2d   replaces Fill_GPU_impl            (src/hydrogen/blas/gpu/Fill.cu:55-76)
+ * hadamard replaces Hadamard_GPU_impl        (src/hydrogen/blas/gpu/Hadamard.cu:62-117)
+ * entrywise_map replaces EntrywiseMapImpl    (include/hydrogen/blas/gpu/EntrywiseMapImpl.hpp:36-211) */
+int elx_axpy2d(int dtype, int64_t m, int64_t n, double alpha,
+               const void* X, int64_t xcs, int64_t xrs,
+               void* Y, int64_t ycs, int64_t yrs, void* stream);
+int elx_copy2d(int dtype, int64_t m, int64_t n,
+               const void* A, int64_t acs, int64_t ars,
+               void* B, int64_t bcs, int64_t brs, void* stream);
+int elx_transpose(int dtype, int64_t m, int64_t n,
+                  const void* A, int64_t lda, void* B, int64_t ldb, void* stream);
+int elx_scale2d(int dtype, int64_t m, int64_t n, double alpha,
+                void* A, int64_t lda, void* stream);
+int elx_fill2d(int dtype, int64_t m, int64_t n, double value,
+               void* A, int64_t lda, void* stream);
+int elx_hadamard2d(int dtype, int64_t m, int64_t n,
+                   const void* A, int64_t lda, const void* B, int64_t ldb,
+                   void* C, int64_t ldc, void* stream);
+int elx_entrywise_map(int dtype, int fn, int64_t m, int64_t n,
+                      const void* A, int64_t lda, void* B, int64_t ldb, void* stream);
+/* grid-independent synthetic fill: A(i,j) = center + radius*u(seed,i0+i,j0+j), u in [-1,1) */
+int elx_fill_hash(int dtype, int64_t m, int64_t n, void* A, int64_t lda,
+                  int64_t i0, int64_t istride, int64_t j0, int64_t jstride,
+                  uint64_t seed, double center, double radius, void* stream);
+
+/* ---- communication: replaces El::mpi::{AllGather,ReduceScatter,AllToAll,
+ * SendRecv,Broadcast,Barrier} + Aluminum (src/core/imports/mpi/{AllGather,ReduceScatter,...}.hpp,
+ * include/El/core/imports/aluminum.hpp:24-365).  Backend: RCCL over xGMI for
+ * device buffers, or a caller-supplied host collective (e.g. a gloo bridge). */
+typedef struct elx_comm_s* elx_comm_t;
+#define ELX_COLL_ALLGATHER      0  /* recv[r*count..] = send of rank r           */
+#define ELX_COLL_REDUCE_SCATTER 1  /* recv = sum_r send_r[me*count..]           */
+#define ELX_COLL_ALLTOALL       2  /* recv[r*count..] = send_r[me*count..]      */
+#define ELX_COLL_SENDRECV       3  /* send -> peer, recv <- peer2               */
+#define ELX_COLL_BCAST          4  /* buffer (send==recv) from root=peer        */
+#define ELX_COLL_ALLREDUCE      5  /* recv = sum_r send_r                        */
+#define ELX_COLL_BARRIER        6
+/* host collective callback; count is in ELEMENTS of dtype, buffers are host
+ * memory, `group` is an opaque id returned by the split callback (0 = world). */
+typedef int (*elx_host_coll_fn)(void* ctx, int op, int group, int dtype,
+                                const void* send, void* recv, int64_t count,
+                                int peer, int peer2);
+/* host split callback: collective over `group` (the library only splits the
+ * world, group 0); returns the new group's id, this rank's rank and its size */
+typedef int (*elx_host_split_fn)(void* ctx, int group, int color, int key,
+                                 int* out_group, int* out_rank, int* out_size);
+int elx_comm_unique_id(unsigned char id[128]);
+int elx_comm_init_rccl(elx_comm_t* world, int rank, int size, const unsigned char id[128]);
+int elx_comm_init_host(elx_comm_t* world, int rank, int size,
+                       elx_host_coll_fn coll, elx_host_split_fn split, void* ctx);
+int elx_comm_rank(elx_comm_t comm, int* rank);
+int elx_comm_size(elx_comm_t comm, int* size);
+int elx_comm_destroy(elx_comm_t comm);
+/* raw typed collectives on device (RCCL) or host (callback) buffers, on `stream` */
+int elx_comm_allgather(elx_comm_t comm, int dtype, const void* send, void* recv,
+                       int64_t count, void* stream);
+int elx_comm_reduce_scatter(elx_comm_t comm, int dtype, const void* send, void* recv,
+                            int64_t count, void* stream);
+int elx_comm_barrier(elx_comm_t comm);
+/* cumulative traffic counters of the collectives issued by this process */
+int elx_comm_stats(int64_t* bytes_moved, double* seconds, int64_t* calls);
+int elx_comm_stats_reset(void);
+
+/* ---- El::Grid (src/core/Grid.cpp:58-206) --------------------------------- */
+typedef struct elx_grid_s* elx_grid_t;
+int elx_grid_default_height(int size);                 /* Grid::DefaultHeight */
+int elx_grid_create(elx_grid_t* grid, elx_comm_t world, int height, int order);
+/* info[0..7] = height, width, size, rank(VC), mcRank, mrRank, vcRank, vrRank */
+int elx_grid_info(elx_grid_t grid, int* info);
+int elx_grid_destroy(elx_grid_t grid);
+
+/* ---- El::DistMatrix<T,U,V,ELEMENT,D> (include/El/core/DistMatrix/, src/core/DistMatrix/) */
+typedef struct elx_dm_s* elx_dm_t;
+int elx_dm_create(elx_dm_t* A, elx_grid_t grid, int dtype, int coldist, int rowdist,
+                  int device, int root);
+int elx_dm_destroy(elx_dm_t A);
+int elx_dm_align(elx_dm_t A, int colAlign, int rowAlign, int constrain);
+int elx_dm_align_with(elx_dm_t A, elx_dm_t B, int constrain);
+int elx_dm_resize(elx_dm_t A, int64_t height, int64_t width);
+/* info[0..12] = height, width, localHeight, localWidth, ldim, colAlign, rowAlign,
+ *               colShift, rowShift, colStride, rowStride, participating, viewing */
+int elx_dm_info(elx_dm_t A, int64_t* info);
+int elx_dm_buffer(elx_dm_t A, void** ptr);
+/* host <-> local buffer (column-major, leading dim ld) */
+int elx_dm_set_local(elx_dm_t A, const void* host, int64_t ld);
+int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld);
+/* V := A(i0:i1, j0:j1) (a view, El::View / A(IR,IR)) */
+int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1);
+/* B := A  (DistMatrix::operator=, the redistribution dispatch table,
+ * src/core/DistMatrix/ElementMatrix/{MC_MR,MC_STAR,...}.cpp); bit-exact */
+int elx_dm_copy(elx_dm_t B, elx_dm_t A);
+/* B := A^T (El::Transpose, include/El/blas_like/level1/Transpose.hpp:191-250) */
+int elx_dm_transpose(elx_dm_t A, elx_dm_t B);
+/* synthetic grid-independent fill from global indices (see elx_fill_hash) */
+int elx_dm_fill_hash(elx_dm_t A, uint64_t seed, double center, double radius);
+int elx_dm_synchronize(elx_dm_t A);
+
+/* ---- distributed BLAS-1 front doors (include/El/blas_like/level1/) ---- */
+int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y);       /* Axpy.hpp:151-176     */
+int elx_dm_scale(double alpha, elx_dm_t A);                   /* Scale.hpp:18-31      */
+int elx_dm_zero(elx_dm_t A);                                  /* Zero.hpp             */
+int elx_dm_hadamard(elx_dm_t A, elx_dm_t B, elx_dm_t C);      /* Hadamard.hpp:107-131 */
+int elx_dm_entrywise_map(int fn, elx_dm_t A, elx_dm_t B);     /* EntrywiseMap.hpp:90-137 */
+/* reduce-scatter family: B += alpha * contract(A)  (AxpyContract.hpp:483-544) */
+int elx_dm_axpy_contract(double alpha, elx_dm_t A, elx_dm_t B);
+
+/* ---- Level 3: El::Gemm / El::LocalGemm (src/blas_like/level3/Gemm.cpp:273-426) */
+int elx_gemm(int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t B,
+             double beta, elx_dm_t C, int alg);
+int elx_local_gemm(int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t B,
+                   double beta, elx_dm_t C);
+/* Blocksize stack (src/core/environment.cpp:315: default 128) */
+int elx_set_blocksize(int64_t nb);
+int64_t elx_blocksize(void);
+/* compute panel: how many communicated panels are fused into one local MFMA
+ * update (0 = automatic). Changes only the summation order (normwise tol). */
+int elx_set_compute_panel(int64_t kpanel);
+/* algorithm the last elx_gemm call actually ran (after the heuristic) */
+int elx_last_gemm_algorithm(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ELEMENTAL_AMD_H */

@@ -1,0 +1,194 @@
+"""Python handle on the CPU oracle (oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+always as the checker; the product (elemental_amd) never imports it.
+Parity-pinning status: see the header of oracle.c and DESIGN.md §Oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_char, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+MC, MD, MR, VC, VR, STAR, CIRC = range(7)
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        i64, d = c_int64, c_double
+        L.orc_shift.restype = i64
+        L.orc_shift.argtypes = [i64, i64, i64]
+        L.orc_length.restype = i64
+        L.orc_length.argtypes = [i64, i64, i64]
+        L.orc_max_length.restype = i64
+        L.orc_max_length.argtypes = [i64, i64]
+        L.orc_default_height.restype = c_int
+        L.orc_default_height.argtypes = [c_int]
+        L.orc_dist_stride.restype = c_int
+        L.orc_dist_stride.argtypes = [c_int, c_int, c_int]
+        L.orc_dist_rank.restype = c_int
+        L.orc_dist_rank.argtypes = [c_int, c_int, c_int, c_int, c_int]
+        L.orc_local_block.restype = None
+        L.orc_local_block.argtypes = [c_void_p, i64, i64, i64, i64, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, c_int, c_void_p, i64, POINTER(i64), POINTER(i64)]
+        L.orc_place_block.restype = None
+        L.orc_place_block.argtypes = [c_void_p, i64, i64, i64, i64, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, c_int, c_void_p, i64]
+        L.orc_hash_unit.restype = d
+        L.orc_hash_unit.argtypes = [c_uint64, i64, i64]
+        L.orc_hash_fill_f64.restype = None
+        L.orc_hash_fill_f64.argtypes = [i64, i64, c_uint64, d, d, c_void_p, i64]
+        L.orc_hash_fill_f32.restype = None
+        L.orc_hash_fill_f32.argtypes = [i64, i64, c_uint64, d, d, c_void_p, i64]
+        L.orc_gemm_f64.restype = None
+        L.orc_gemm_f64.argtypes = [c_char, c_char, i64, i64, i64, d, c_void_p, i64, c_void_p, i64, d, c_void_p, i64]
+        L.orc_gemm_f32.restype = None
+        L.orc_gemm_f32.argtypes = [c_char, c_char, i64, i64, i64, c_float, c_void_p, i64, c_void_p, i64, c_float,
+                                   c_void_p, i64]
+        L.orc_summa_nnc_f64.restype = None
+        L.orc_summa_nnc_f64.argtypes = [c_int, c_int, i64, i64, i64, i64, d, c_void_p, i64, c_void_p, i64, d,
+                                        c_void_p, i64]
+        L.orc_fro.restype = d
+        L.orc_fro.argtypes = [i64, i64, c_void_p, i64]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(c_void_p)
+
+
+# ------------------------------------------------------------------ layout
+def shift(rank, align, stride):
+    return lib().orc_shift(rank, align, stride)
+
+
+def length(n, shift_, stride):
+    return lib().orc_length(n, shift_, stride)
+
+
+def local_block(G: np.ndarray, U: int, V: int, r: int, c: int, vc: int, col_align=0, row_align=0,
+                root=0) -> np.ndarray:
+    """Local block of global column-major G on VC rank vc for [U,V] (bit copy)."""
+    G = np.asfortranarray(G)
+    H, W = G.shape
+    out = np.zeros((max(H, 1), max(W, 1)), dtype=G.dtype, order="F")
+    lh, lw = c_int64(), c_int64()
+    lib().orc_local_block(_p(G), G.itemsize, H, W, max(H, 1), U, V, r, c, vc, col_align, row_align, root,
+                          _p(out), out.shape[0], ctypes.byref(lh), ctypes.byref(lw))
+    return np.asfortranarray(out[:lh.value, :lw.value])
+
+
+def place_block(G: np.ndarray, loc: np.ndarray, U, V, r, c, vc, col_align=0, row_align=0, root=0):
+    H, W = G.shape
+    loc = np.asfortranarray(loc, dtype=G.dtype)
+    lib().orc_place_block(_p(G), G.itemsize, H, W, max(H, 1), U, V, r, c, vc, col_align, row_align, root,
+                          _p(loc), max(loc.shape[0], 1))
+
+
+# ------------------------------------------------------------------ inputs
+def hash_matrix(H: int, W: int, seed: int, center=0.0, radius=1.0, dtype=np.float64) -> np.ndarray:
+    """Global matrix identical to elx_fill_hash / DistMatrix.fill_hash."""
+    G = np.zeros((H, W), dtype=np.float64, order="F")
+    if H and W:
+        lib().orc_hash_fill_f64(H, W, seed, center, radius, _p(G), H)
+    if dtype == np.float64:
+        return G
+    if dtype == np.float32:
+        return G.astype(np.float32)
+    if dtype == np.float16:  # double -> float (RNE) -> half (RNE), as the device does
+        return G.astype(np.float32).astype(np.float16)
+    if dtype == "bf16":
+        return f32_to_bf16_bits(G.astype(np.float32))
+    raise ValueError(dtype)
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    u = np.asarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    nan = np.isnan(np.asarray(x, dtype=np.float32))
+    r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
+    return np.asfortranarray(r)
+
+
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+# -------------------------------------------------------------------- gemm
+def gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """C := alpha op(A) op(B) + beta C with the reference's loop nest (f64/f32)."""
+    C = np.array(C, order="F", copy=True)
+    A = np.asfortranarray(A)
+    B = np.asfortranarray(B)
+    m, n = C.shape
+    k = A.shape[1] if ta == "N" else A.shape[0]
+    f = lib().orc_gemm_f64 if C.dtype == np.float64 else lib().orc_gemm_f32
+    f(ta.encode(), tb.encode(), m, n, k, alpha, _p(A), max(A.shape[0], 1), _p(B), max(B.shape[0], 1), beta,
+      _p(C), max(m, 1))
+    return C
+
+
+def gemm_half(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """The reference's CPU half path: the naive loops of
+    src/core/imports/blas/Gemm.hpp:47-260 with every operation rounded to half
+    (half_float semantics), vectorised over i."""
+    h = np.float16
+    A = A.astype(h)
+    B = B.astype(h)
+    C = np.array(C, dtype=h, order="F", copy=True)
+    m, n = C.shape
+    k = A.shape[1] if ta == "N" else A.shape[0]
+    al, be = h(alpha), h(beta)
+    if be == h(0):
+        C[:] = h(0)
+    elif be != h(1):
+        C *= be
+    opB = (lambda l, j: B[l, j]) if tb == "N" else (lambda l, j: B[j, l])
+    for j in range(n):
+        if ta == "N":
+            for l in range(k):
+                gamma = h(al * opB(l, j))
+                C[:, j] = (C[:, j] + (A[:, l] * gamma).astype(h)).astype(h)
+        else:
+            for i in range(m):
+                g = h(0)
+                for l in range(k):
+                    g = h(g + h(A[l, i] * opB(l, j)))
+                C[i, j] = h(C[i, j] + h(g * al))
+    return C
+
+
+def summa_nnc(r: int, c: int, nb: int, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """SUMMA_NNC_impl simulated over an r x c grid (oracle.c:orc_summa_nnc_f64)."""
+    C = np.array(C, dtype=np.float64, order="F", copy=True)
+    A = np.asfortranarray(A, dtype=np.float64)
+    B = np.asfortranarray(B, dtype=np.float64)
+    m, n = C.shape
+    k = A.shape[1]
+    lib().orc_summa_nnc_f64(r, c, m, n, k, nb, alpha, _p(A), max(m, 1), _p(B), max(k, 1), beta, _p(C), max(m, 1))
+    return C
+
+
+def parity_ratio(C: np.ndarray, Cref: np.ndarray, A: np.ndarray, B: np.ndarray, k: int, eps: float) -> float:
+    """north_star metric ||C - Cref||_F / (||A||_F ||B||_F k eps)."""
+    num = np.linalg.norm((np.asarray(C, np.float64) - np.asarray(Cref, np.float64)).ravel())
+    den = np.linalg.norm(np.asarray(A, np.float64).ravel()) * np.linalg.norm(np.asarray(B, np.float64).ravel())
+    den *= max(k, 1) * eps
+    return float(num / den) if den > 0 else float(num)

@@ -1,0 +1,170 @@
+"""Multi-rank workers for the CPU (gloo) and GPU (host-staged) distributed tests.
+
+Each worker builds El::Grid over a host-collective bridge (torch.distributed
+gloo), runs the library's redistribution engine / SUMMA drivers on its local
+blocks and checks ONLY its own local block against the oracle's extraction
+of the same global result — exactly what the reference's own tests do
+(tests/core/DistMatrix.cpp:12-78, tests/blas_like/Gemm.cpp:15-49), but
+against an oracle instead of self-consistency.
+"""
+from __future__ import annotations
+
+import os
+import random
+import traceback
+
+import numpy as np
+
+ORIENTS = {0: "N", 1: "T", 2: "T"}
+
+
+def init(rank: int, world: int, port: int):
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from elemental_amd import el
+    from elemental_amd.torch_bridge import GlooBridge
+    bridge = GlooBridge()
+    return el, el.Comm.host(bridge)
+
+
+def finish():
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _bits(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a)
+    return a.view({8: np.uint64, 4: np.uint32, 2: np.uint16}[a.itemsize])
+
+
+def redist_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, m: int, n: int,
+                  seed: int):
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = {el.F64: np.float64, el.F32: np.float32, el.F16: np.float16, el.BF16: "bf16"}[dtype]
+        G = oracle.hash_matrix(m, n, seed, 0.0, 5.0, npdt)
+        rng = random.Random(seed)  # same sequence on every rank
+        pairs = el.VALID_DISTS
+        for (U, V) in pairs:
+            ca = rng.randrange(oracle.lib().orc_dist_stride(U, r, c))
+            ra = rng.randrange(oracle.lib().orc_dist_stride(V, r, c))
+            A = el.DistMatrix(g, dtype, U, V, device, root=world - 1)
+            A.Align(ca, ra)
+            A.Resize(m, n)
+            A.set_local(oracle.local_block(G, U, V, r, c, g.vc_rank, ca, ra, world - 1))
+            for (X, Y) in pairs:
+                xa = rng.randrange(oracle.lib().orc_dist_stride(X, r, c))
+                ya = rng.randrange(oracle.lib().orc_dist_stride(Y, r, c))
+                B = el.DistMatrix(g, dtype, X, Y, device, root=rng.randrange(world))
+                B.Align(xa, ya)
+                B.assign(A)
+                want = oracle.local_block(G, X, Y, r, c, g.vc_rank, xa, ya, B.root)
+                got = B.get_local()
+                tag = f"[{el.DIST_NAMES[X]},{el.DIST_NAMES[Y]}]({xa},{ya}) <- " \
+                      f"[{el.DIST_NAMES[U]},{el.DIST_NAMES[V]}]({ca},{ra}) grid {r}x{c} rank {rank}"
+                assert got.shape == want.shape, f"{tag}: shape {got.shape} vs {want.shape}"
+                assert np.array_equal(_bits(got), _bits(want)), f"{tag}: data mismatch"
+                # an unconstrained target adopts an alignment and still holds the matrix
+                B2 = el.DistMatrix(g, dtype, X, Y, device)
+                B2.assign(A)
+                i = B2.info()
+                want2 = oracle.local_block(G, X, Y, r, c, g.vc_rank, i["col_align"], i["row_align"], 0)
+                assert np.array_equal(_bits(B2.get_local()), _bits(want2)), f"{tag}: unconstrained target"
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def _tol(dtype):
+    return {0: np.finfo(np.float32).eps, 1: np.finfo(np.float64).eps}[dtype]
+
+
+def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, algs,
+                nb: int, seed: int):
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = np.float64 if dtype == el.F64 else np.float32
+        el.SetBlocksize(nb)
+        el.SetComputePanel(0)
+        for (m, n, k) in shapes:
+            for oA in (el.NORMAL, el.TRANSPOSE):
+                for oB in (el.NORMAL, el.TRANSPOSE):
+                    Ag = oracle.hash_matrix(m if oA == 0 else k, k if oA == 0 else m, seed + 1, -0.1, 0.1, npdt)
+                    Bg = oracle.hash_matrix(k if oB == 0 else n, n if oB == 0 else k, seed + 2, -0.1, 0.1, npdt)
+                    Cg = oracle.hash_matrix(m, n, seed + 3, -0.1, 0.1, npdt)
+                    alpha, beta = 0.5, -0.5  # Gemm_Suite.cpp:158-172
+                    ref = oracle.gemm(ORIENTS[oA], ORIENTS[oB], alpha, Ag, Bg, beta, Cg)
+                    for alg in algs:
+                        A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Ag.shape[0], width=Ag.shape[1])
+                        B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Bg.shape[0], width=Bg.shape[1])
+                        C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
+                        A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+                        B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
+                        C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                        ran = el.Gemm(oA, oB, alpha, A, B, beta, C, alg)
+                        got = C.get_local().astype(np.float64)
+                        want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
+                        # north_star normwise bound, applied blockwise with the global norms
+                        num = np.linalg.norm(got - want) if got.size else 0.0
+                        den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) \
+                            * max(k, 1) * _tol(dtype)
+                        assert num <= 10 * den, (f"Gemm {ORIENTS[oA]}{ORIENTS[oB]} alg {alg}->{ran} "
+                                                 f"{m}x{n}x{k} grid {r}x{c} rank {rank}: {num / den:.3g}")
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def blas1_worker(rank: int, world: int, port: int, height: int, device: int, seed: int):
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        m, n = 23, 17
+        Xg = oracle.hash_matrix(m, n, seed, 0.0, 1.0)
+        Yg = oracle.hash_matrix(m, n, seed + 1, 0.0, 1.0)
+        # Axpy across distributions: Y[MC,MR] += 2 X[VC,STAR]
+        X = el.DistMatrix(g, el.F64, el.VC, el.STAR, device, height=m, width=n)
+        X.set_local(oracle.local_block(Xg, el.VC, el.STAR, r, c, g.vc_rank))
+        Y = el.DistMatrix(g, el.F64, el.MC, el.MR, device, height=m, width=n)
+        Y.set_local(oracle.local_block(Yg, el.MC, el.MR, r, c, g.vc_rank))
+        el.Axpy(2.0, X, Y)
+        want = oracle.local_block(Yg + 2.0 * Xg, el.MC, el.MR, r, c, g.vc_rank)
+        assert np.array_equal(Y.get_local(), want), "Axpy"
+        # Hadamard on [MC,MR]
+        Z = el.DistMatrix(g, el.F64, el.MC, el.MR, device)
+        Yc = el.DistMatrix(g, el.F64, el.MC, el.MR, device, height=m, width=n)
+        Yc.set_local(oracle.local_block(Yg, el.MC, el.MR, r, c, g.vc_rank))
+        Xm = el.DistMatrix(g, el.F64, el.MC, el.MR, device, height=m, width=n)
+        Xm.set_local(oracle.local_block(Xg, el.MC, el.MR, r, c, g.vc_rank))
+        el.Hadamard(Xm, Yc, Z)
+        assert np.array_equal(Z.get_local(), oracle.local_block(Xg * Yg, el.MC, el.MR, r, c, g.vc_rank)), "Hadamard"
+        # AxpyContract: [MC,*] partial sums over MR -> [MC,MR]
+        D = el.DistMatrix(g, el.F64, el.MC, el.STAR, device, height=m, width=n)
+        D.set_local(oracle.local_block(Xg, el.MC, el.STAR, r, c, g.vc_rank) * (g.mr_rank + 1))
+        E = el.DistMatrix(g, el.F64, el.MC, el.MR, device, height=m, width=n)
+        E.set_local(oracle.local_block(Yg, el.MC, el.MR, r, c, g.vc_rank))
+        el.AxpyContract(1.0, D, E)
+        tot = sum(range(1, c + 1))
+        want = oracle.local_block(Yg + tot * Xg, el.MC, el.MR, r, c, g.vc_rank)
+        assert np.allclose(E.get_local(), want, rtol=0, atol=1e-13), "AxpyContract"
+        # EntrywiseMap into another distribution
+        F = el.DistMatrix(g, el.F64, el.STAR, el.VR, device)
+        el.EntrywiseMap(el.L.MAP_SQUARE if hasattr(el, "L") else 3, Xm, F)
+        want = oracle.local_block(Xg * Xg, el.STAR, el.VR, r, c, g.vc_rank, 0, F.RowAlign())
+        assert np.array_equal(F.get_local(), want), "EntrywiseMap"
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise

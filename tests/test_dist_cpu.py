@@ -1,0 +1,49 @@
+"""Multi-rank CPU tests (gloo, world sizes 2 and 4): the SAME C++ redistribution
+engine and SUMMA drivers that run on RCCL, on Device::CPU matrices over a
+host-collective bridge.  Grids 1x2, 2x1, 2x2."""
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import _dist_workers as W
+from elemental_amd import el
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(fn, world, *args):
+    mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (2, 2), (4, 2)])
+def test_redistribution_all_pairs_bit_exact(world, height):
+    """tests/core/DistMatrix.cpp: every [X,Y] <- [U,V] with random alignments."""
+    _spawn(W.redist_worker, world, height, el.CPU, el.F64, 13, 11, 1234 + world + height)
+
+
+def test_redistribution_f16_bit_exact():
+    _spawn(W.redist_worker, 2, 1, el.CPU, el.F16, 9, 7, 99)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_gemm_all_orientations_all_algorithms(world, height):
+    """SUMMA A/B/C/Dot x NN/NT/TN/TT against the oracle (north_star tolerance)."""
+    algs = [el.GEMM_DEFAULT, el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT,
+            el.GEMM_SUMMA_C_MS]
+    _spawn(W.gemm_worker, world, height, el.CPU, el.F64, [(19, 13, 23), (8, 9, 40)], algs, 4, 7)
+
+
+def test_gemm_f32_grid_2x2():
+    _spawn(W.gemm_worker, 4, 2, el.CPU, el.F32, [(17, 21, 15)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 4, 11)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_blas1_distributed(world, height):
+    _spawn(W.blas1_worker, world, height, el.CPU, 5)
