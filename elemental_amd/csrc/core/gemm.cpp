@@ -25,6 +25,7 @@
 #include "redist.hpp"
 #include "exec.hpp"
 #include <algorithm>
+#include <vector>
 
 namespace elx {
 
@@ -35,6 +36,35 @@ int g_last_alg = ELX_GEMM_DEFAULT;
 constexpr Int kDotBlock = 2000;  // NN.hpp:578 (hard-coded in the reference)
 
 bool IsN(int o) { return o == ELX_NORMAL; }
+
+// Event-bracketed profiling of the local updates and panel transfers.
+struct Profiler {
+    struct Rec { hipEvent_t a, b; double work; };
+    bool on = false;
+    std::vector<Rec> gemm, comm;
+    void Clear() {
+        for (auto* v : {&gemm, &comm})
+            for (auto& r : *v) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        gemm.clear();
+        comm.clear();
+    }
+    Rec Begin(hipStream_t s) {
+        Rec r{};
+        ELX_CHECK_HIP(hipEventCreate(&r.a));
+        ELX_CHECK_HIP(hipEventCreate(&r.b));
+        ELX_CHECK_HIP(hipEventRecord(r.a, s));
+        return r;
+    }
+    void End(Rec r, hipStream_t s, double work, std::vector<Rec>& into) {
+        ELX_CHECK_HIP(hipEventRecord(r.b, s));
+        r.work = work;
+        into.push_back(r);
+    }
+};
+Profiler& Prof() {
+    static Profiler p;
+    return p;
+}
 
 void FenceStreams(hipStream_t from, hipStream_t to) {
     if (!from || !to || from == to) return;
@@ -144,12 +174,17 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         auto Bv = IsN(oB) ? DistMatrix::View(B, k0, k1, 0, B.Width()) : DistMatrix::View(B, 0, B.Height(), k0, k1);
         Av->SetStream(ms);
         Bv->SetStream(ms);
+        const bool prof = gpu && Prof().on;
+        Profiler::Rec rec{};
+        const int64_t bytes0 = GlobalCommStats().bytes;
+        if (prof) rec = Prof().Begin(ms);
         // a panel whose local block already IS the gathered layout (e.g. every
         // panel on a 1x1 grid) is used in place: no copy at all
         if (SameLocalLayout(*Av, a_cd, a_rd, s.a->ColAlign(), s.a->RowAlign())) s.ua = Av;
         else { Copy(*Av, *s.a); s.ua = s.a; }
         if (SameLocalLayout(*Bv, b_cd, b_rd, s.b->ColAlign(), s.b->RowAlign())) s.ub = Bv;
         else { Copy(*Bv, *s.b); s.ub = s.b; }
+        if (prof) Prof().End(rec, ms, static_cast<double>(GlobalCommStats().bytes - bytes0), Prof().comm);
         if (gpu) ELX_CHECK_HIP(hipEventRecord(s.ready, ms));
     };
     auto compute = [&](int p) {
@@ -159,9 +194,14 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         if (gpu) ELX_CHECK_HIP(hipStreamWaitEvent(cs, s.ready, 0));
         const Int m = C.LocalHeight(), n = C.LocalWidth();
         const Int k = IsN(oA) ? a.LocalWidth() : a.LocalHeight();
-        if (m > 0 && n > 0 && k > 0)
+        if (m > 0 && n > 0 && k > 0) {
+            const bool prof = gpu && Prof().on;
+            Profiler::Rec rec{};
+            if (prof) rec = Prof().Begin(cs);
             exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(), b.LDim(),
                        1.0, C.Buffer(), C.LDim(), cs);
+            if (prof) Prof().End(rec, cs, 2.0 * m * n * k, Prof().gemm);
+        }
         if (gpu) {
             ELX_CHECK_HIP(hipEventRecord(s.done, cs));
             s.pending = true;
@@ -314,6 +354,32 @@ void SetComputePanel(Int kc) { ELX_REQUIRE(kc >= 0, "compute panel must be >= 0"
 Int ComputePanel() { return g_compute_panel; }
 int LastGemmAlgorithm() { return g_last_alg; }
 
+void SetProfiling(bool on) {
+    if (Runtime::Get().GPUInitialized()) ELX_CHECK_HIP(hipDeviceSynchronize());
+    Prof().Clear();
+    Prof().on = on;
+}
+
+void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& comm_ms, int64_t& bytes) {
+    gemm_ms = comm_ms = flops = 0;
+    launches = bytes = 0;
+    if (!Runtime::Get().GPUInitialized()) return;
+    ELX_CHECK_HIP(hipDeviceSynchronize());
+    for (auto& r : Prof().gemm) {
+        float ms = 0;
+        ELX_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        gemm_ms += ms;
+        flops += r.work;
+        ++launches;
+    }
+    for (auto& r : Prof().comm) {
+        float ms = 0;
+        ELX_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        comm_ms += ms;
+        bytes += static_cast<int64_t>(r.work);
+    }
+}
+
 void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C) {
     ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "LocalGemm: mixed types");
     ELX_REQUIRE(A.Dev() == B.Dev() && A.Dev() == C.Dev(), "LocalGemm: mixed devices");
@@ -334,12 +400,16 @@ void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatr
         Scale(beta, C);
         return;
     }
+    const bool prof = C.Dev() == Device::GPU && Prof().on;
+    Profiler::Rec rec{};
     if (C.Dev() == Device::GPU) {
         FenceStreams(A.Stream(), C.Stream());
         FenceStreams(B.Stream(), C.Stream());
+        if (prof) rec = Prof().Begin(C.Stream());
     }
     exec::Gemm(C.Dev(), C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
                beta, C.Buffer(), C.LDim(), C.Stream());
+    if (prof) Prof().End(rec, C.Stream(), 2.0 * m * n * k, Prof().gemm);
 }
 
 void LocalGemmResize(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, DistMatrix& C) {

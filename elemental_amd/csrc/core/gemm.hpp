@@ -19,5 +19,7 @@ Int Blocksize();
 void SetComputePanel(Int kc);
 Int ComputePanel();
 int LastGemmAlgorithm();
+void SetProfiling(bool on);
+void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& comm_ms, int64_t& bytes);
 
 }  // namespace elx

@@ -151,7 +151,8 @@ __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>
     using E = Elem<T>;
     for_each_2d(m, n, [&](i64 i, i64 j) {
         const double u = hash_unit(seed, i0 + i * istride, j0 + j * jstride);
-        const double v = center + radius * (2.0 * u - 1.0);
+        // explicit roundings: no FMA contraction, so host and device agree bit for bit
+        const double v = __dadd_rn(center, __dmul_rn(radius, __dsub_rn(__dmul_rn(2.0, u), 1.0)));
         A[i + j * lda] = E::store((typename E::compute)v);  // double -> compute (RNE) -> storage (RNE)
     });
 }

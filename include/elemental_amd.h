@@ -248,6 +248,13 @@ int64_t elx_blocksize(void);
 int elx_set_compute_panel(int64_t kpanel);
 /* algorithm the last elx_gemm call actually ran (after the heuristic) */
 int elx_last_gemm_algorithm(void);
+/* Profiling (replaces AUTO_PROFILE_REGION/NVTX ranges, include/El/core/Profiling.hpp:143-264):
+ * when on, every local MFMA update and every panel transfer issued by the SUMMA
+ * drivers is bracketed by HIP events on the stream it runs on.  stats: summed
+ * kernel ms, launches, algorithmic FLOPs; summed transfer ms and bytes moved. */
+int elx_set_profiling(int on);
+int elx_profile_stats(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops,
+                      double* comm_ms, int64_t* comm_bytes);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,200 @@
+"""gfx950 kernel parity through the C-ABI (local GEMM, BLAS-1, hash fill)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from elemental_amd import _lib as L
+from elemental_amd import el
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def dev(a: np.ndarray) -> "torch.Tensor":
+    """Column-major host array -> device tensor holding the same bytes."""
+    a = np.asfortranarray(a)
+    flat = np.ravel(a, order="F")
+    if flat.dtype == np.uint16:
+        flat = flat.view(np.int16)
+    return torch.from_numpy(flat.copy()).cuda()
+
+
+def host(t, shape, dtype):
+    torch.cuda.synchronize()
+    a = t.cpu().numpy()
+    if dtype == np.uint16:
+        a = a.view(np.uint16)
+    return np.asfortranarray(a.reshape(shape, order="F"))
+
+
+def sync():
+    L.call("elx_device_synchronize")
+    torch.cuda.synchronize()
+
+
+OPS = {"N": L.NORMAL, "T": L.TRANSPOSE}
+SHAPES = [(1, 1, 1), (67, 53, 41), (128, 128, 16), (255, 257, 130), (300, 200, 517), (16, 700, 3)]
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+def test_local_gemm_f64_f32(dt, ta, tb):
+    npdt = np.float64 if dt == "f64" else np.float32
+    eps = np.finfo(npdt).eps
+    fn = L.lib().elx_gemm_f64 if dt == "f64" else L.lib().elx_gemm_f32
+    for (m, n, k) in SHAPES:
+        for beta in (0.0, -0.5):
+            A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 11, 0, 1, npdt)
+            B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 12, 0, 1, npdt)
+            C = oracle.hash_matrix(m, n, 13, 0, 1, npdt)
+            if beta == 0.0:
+                C[:] = np.nan  # beta == 0 must never read C
+            ref = oracle.gemm(ta, tb, 0.5, A, B, beta, np.nan_to_num(C))
+            dA, dB, dC = dev(A), dev(B), dev(C)
+            torch.cuda.synchronize()
+            L.check(fn(OPS[ta], OPS[tb], m, n, k, 0.5, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0],
+                       beta, dC.data_ptr(), m, None))
+            sync()
+            got = host(dC, (m, n), npdt)
+            assert np.isfinite(got).all()
+            r = oracle.parity_ratio(got, ref, A, B, k, eps)
+            assert r <= 10, f"{dt} {ta}{tb} {m}x{n}x{k} beta={beta}: ratio {r}"
+
+
+def test_local_gemm_known_answer_exact():
+    """Integer-valued operands: every partial sum is exact in fp64, so the
+    product must match bit for bit whatever the summation order."""
+    rng = np.random.default_rng(0)
+    m, n, k = 130, 70, 300
+    A = np.asfortranarray(rng.integers(-8, 8, (m, k)).astype(np.float64))
+    B = np.asfortranarray(rng.integers(-8, 8, (k, n)).astype(np.float64))
+    C = np.asfortranarray(rng.integers(-8, 8, (m, n)).astype(np.float64))
+    dA, dB, dC = dev(A), dev(B), dev(C)
+    torch.cuda.synchronize()
+    L.call("elx_gemm_f64", 0, 0, m, n, k, 2.0, dA.data_ptr(), m, dB.data_ptr(), k, -1.0, dC.data_ptr(), m, None)
+    sync()
+    assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * A @ B - C)
+
+
+@pytest.mark.parametrize("kind", ["f16", "bf16"])
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+def test_local_gemm_16bit(kind, ta, tb):
+    m, n, k = 131, 77, 95
+    if kind == "f16":
+        A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 21, 0, 1, np.float16)
+        B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 22, 0, 1, np.float16)
+        C = oracle.hash_matrix(m, n, 23, 0, 1, np.float16)
+        Af, Bf, Cf = A.astype(np.float64), B.astype(np.float64), C.astype(np.float64)
+        fn, eps, hostdt = L.lib().elx_gemm_f16, 2.0 ** -11, np.float16
+    else:
+        A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 21, 0, 1, "bf16")
+        B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 22, 0, 1, "bf16")
+        C = oracle.hash_matrix(m, n, 23, 0, 1, "bf16")
+        Af, Bf, Cf = (oracle.bf16_bits_to_f32(x).astype(np.float64) for x in (A, B, C))
+        fn, eps, hostdt = L.lib().elx_gemm_bf16, 2.0 ** -8, np.uint16
+    exact = oracle.gemm(ta, tb, 0.5, Af, Bf, -0.5, Cf)
+    dA, dB, dC = dev(A), dev(B), dev(C)
+    torch.cuda.synchronize()
+    L.check(fn(OPS[ta], OPS[tb], m, n, k, 0.5, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0], -0.5,
+               dC.data_ptr(), m, None))
+    sync()
+    got = host(dC, (m, n), hostdt)
+    gotf = got.astype(np.float64) if kind == "f16" else oracle.bf16_bits_to_f32(got).astype(np.float64)
+    r = oracle.parity_ratio(gotf, exact, Af, Bf, k, eps)
+    assert r <= 10, f"{kind} {ta}{tb}: ratio {r}"
+    if kind == "f16":
+        # never worse than the reference's own CPU half path (half accumulation)
+        refh = oracle.gemm_half(ta, tb, 0.5, A, B, -0.5, C).astype(np.float64)
+        assert np.linalg.norm(gotf - exact) <= np.linalg.norm(refh - exact) + 1e-3
+
+
+DTYPES = [(L.F64, np.float64), (L.F32, np.float32), (L.F16, np.float16), (L.BF16, "bf16")]
+
+
+def _mat(m, n, seed, npdt):
+    return oracle.hash_matrix(m, n, seed, 0.0, 2.0, npdt)
+
+
+def _as_f64(x, npdt):
+    return oracle.bf16_bits_to_f32(x).astype(np.float64) if npdt == "bf16" else x.astype(np.float64)
+
+
+def _round(x, npdt):
+    if npdt == "bf16":
+        return oracle.f32_to_bf16_bits(x.astype(np.float32))
+    return x.astype(npdt)
+
+
+@pytest.mark.parametrize("t,npdt", DTYPES)
+def test_blas1_kernels(t, npdt):
+    hostdt = np.uint16 if npdt == "bf16" else npdt
+    m, n = 77, 45
+    X = _mat(m, n, 31, npdt)
+    Y = _mat(m, n, 32, npdt)
+    Xf, Yf = _as_f64(X, npdt), _as_f64(Y, npdt)
+    # copy2d with a transposing stride pattern: B (n x m) = X^T
+    dX, dB = dev(X), dev(np.zeros((n, m), dtype=hostdt))
+    torch.cuda.synchronize()
+    L.call("elx_transpose", t, m, n, dX.data_ptr(), m, dB.data_ptr(), n, None)
+    sync()
+    assert np.array_equal(host(dB, (n, m), hostdt), np.asfortranarray(X.T))
+    # strided copy: every other row/column
+    dC = dev(np.zeros(((m + 1) // 2, (n + 1) // 2), dtype=hostdt))
+    torch.cuda.synchronize()
+    L.call("elx_copy2d", t, (m + 1) // 2, (n + 1) // 2, dX.data_ptr(), 2, 2 * m, dC.data_ptr(), 1, (m + 1) // 2, None)
+    sync()
+    assert np.array_equal(host(dC, ((m + 1) // 2, (n + 1) // 2), hostdt), np.asfortranarray(X[::2, ::2]))
+    # axpy2d Y += 0.5 X and the transposed form
+    dY = dev(Y)
+    torch.cuda.synchronize()
+    L.call("elx_axpy2d", t, m, n, 0.5, dX.data_ptr(), 1, m, dY.data_ptr(), 1, m, None)
+    sync()
+    got = _as_f64(host(dY, (m, n), hostdt), npdt)
+    want = _as_f64(_round((Yf + 0.5 * Xf) if t in (L.F64,) else (Yf.astype(np.float32) + np.float32(0.5) * Xf.astype(np.float32)), npdt), npdt)
+    assert np.array_equal(got, want)
+    # scale, fill, hadamard, entrywise map
+    dS = dev(X)
+    torch.cuda.synchronize()
+    L.call("elx_scale2d", t, m, n, -2.0, dS.data_ptr(), m, None)
+    sync()
+    assert np.array_equal(_as_f64(host(dS, (m, n), hostdt), npdt), -2.0 * Xf)
+    L.call("elx_fill2d", t, m, n, 0.25, dS.data_ptr(), m, None)
+    sync()
+    assert (_as_f64(host(dS, (m, n), hostdt), npdt) == 0.25).all()
+    dZ = dev(np.zeros((m, n), dtype=hostdt))
+    dY = dev(Y)
+    torch.cuda.synchronize()
+    L.call("elx_hadamard2d", t, m, n, dX.data_ptr(), m, dY.data_ptr(), m, dZ.data_ptr(), m, None)
+    sync()
+    prod = (Xf * Yf) if t == L.F64 else (Xf.astype(np.float32) * Yf.astype(np.float32))
+    assert np.array_equal(_as_f64(host(dZ, (m, n), hostdt), npdt), _as_f64(_round(prod, npdt), npdt))
+    L.call("elx_entrywise_map", t, L.MAP_ABS, m, n, dX.data_ptr(), m, dZ.data_ptr(), m, None)
+    sync()
+    assert np.array_equal(_as_f64(host(dZ, (m, n), hostdt), npdt), np.abs(Xf))
+
+
+@pytest.mark.parametrize("t,npdt", DTYPES)
+def test_fill_hash_bit_exact(t, npdt):
+    hostdt = np.uint16 if npdt == "bf16" else npdt
+    m, n = 300, 129
+    d = dev(np.zeros((m, n), dtype=hostdt))
+    torch.cuda.synchronize()
+    L.call("elx_fill_hash", t, m, n, d.data_ptr(), m, 0, 1, 0, 1, 77, -0.1, 0.1, None)
+    sync()
+    want = oracle.hash_matrix(m, n, 77, -0.1, 0.1, npdt)
+    got = host(d, (m, n), hostdt)
+    assert got.tobytes(order="F") == np.asarray(want, dtype=hostdt).tobytes(order="F")
+
+
+def test_pool_alloc_free():
+    p = ctypes.c_void_p()
+    L.call("elx_pool_alloc", ctypes.byref(p), 1 << 20, None)
+    assert p.value
+    L.call("elx_pool_free", p, None)
+    r, u = el.pool_stats()
+    assert u == 0 or u >= 0
