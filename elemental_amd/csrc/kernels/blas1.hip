@@ -150,9 +150,12 @@ __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>
                                                   double center, double radius) {
     using E = Elem<T>;
     for_each_2d(m, n, [&](i64 i, i64 j) {
+#pragma clang fp contract(off)
         const double u = hash_unit(seed, i0 + i * istride, j0 + j * jstride);
         // explicit roundings: no FMA contraction, so host and device agree bit for bit
-        const double v = __dadd_rn(center, __dmul_rn(radius, __dsub_rn(__dmul_rn(2.0, u), 1.0)));
+        // plain operators under `contract(off)`: the instructions are created in
+        // this scope, so no fused multiply-add can merge them (host == device)
+        const double v = center + radius * (2.0 * u - 1.0);
         A[i + j * lda] = E::store((typename E::compute)v);  // double -> compute (RNE) -> storage (RNE)
     });
 }

@@ -6,19 +6,28 @@
 // (src/blas_like/level3/Gemm.cpp:163-186 LocalGemm -> Gemm_impl<GPU>).
 //
 // Design (MI355X-first):
-//  * 128x128 output tile per 256-thread workgroup, 4 waves of 64x64, each wave a
-//    4x4 grid of 16x16 MFMA accumulators (v_mfma_f64_16x16x4_f64 /
-//    v_mfma_f32_16x16x4_f32: one operand element per lane, so every orientation
-//    shares one LDS image [k][i] / [k][j]).
+//  * One 256-thread workgroup per BM x BN output tile, 4 waves in a 2x2
+//    arrangement; each wave owns (BM/2) x (BN/2) as a grid of 16x16 MFMA
+//    accumulators (v_mfma_f64_16x16x4_f64 / v_mfma_f32_16x16x4_f32: one
+//    operand element per lane, so every orientation shares one LDS image [k][r]).
+//    Two shapes: 128x128 (2 workgroups per CU, 2 waves per SIMD) and 256x128
+//    (1 workgroup per CU, 1 wave per SIMD with 8x4 accumulators in the
+//    unified VGPR/AGPR file, fewer LDS reads and HBM bytes per MFMA).
 //  * BK = 16 k-slab, double-buffered in LDS; the next slab's global loads are
 //    issued into registers before the current slab's MFMAs and written to the
 //    other LDS buffer after them (one barrier per slab).
-//  * LDS row pitch 145 elements: conflict-free for the contiguous (N) staging
-//    writes, <=2-way for the transposed (T) staging writes and the MFMA reads.
+//  * Loads never branch: indices are clamped into the matrix (always a valid
+//    address) and out-of-range elements zeroed by a select at the LDS store,
+//    so the wait for a slab's loads sits after the MFMAs.  With 16-B aligned
+//    operands each lane moves a 16-B pair along the unit-stride dimension, and
+//    offsets inside a slab are 32-bit off a per-slab uniform base.
+//  * LDS pitch: ROWS+16 when r is HBM-contiguous (MFMA reads conflict-free),
+//    ROWS+17 otherwise (the transposing staging writes conflict-free).
 //  * XCD-aware, bijective blockIdx remap + grouped tile order so the 32 CUs of
 //    one XCD work on a compact patch of C and share A/B panels in their L2.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace elx {
 namespace kern {
@@ -27,10 +36,13 @@ using i64 = int64_t;
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct Mfma;
 template <> struct Mfma<double> {
     using acc_t = f64x4;
+    using pair_t = f64x2;
     static __device__ __forceinline__ acc_t op(double a, double b, acc_t c) {
         return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
     }
@@ -39,6 +51,7 @@ template <> struct Mfma<double> {
 };
 template <> struct Mfma<float> {
     using acc_t = f32x4;
+    using pair_t = f32x2;
     static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
     }
@@ -56,8 +69,7 @@ struct GemmParams {
     int tiles_m, tiles_n;
 };
 
-constexpr int BM = 128, BN = 128, BK = 16, NTHR = 256, LDP = 145, GROUP_M = 8;
-constexpr int EPT = BM * BK / NTHR;  // elements per thread per operand per slab = 8
+constexpr int BK = 16, GROUP_M = 8;
 
 // Map the flat workgroup id to a (tile_m, tile_n) pair.  Workgroups are dealt
 // round-robin over the 8 XCDs (b and b+8 share one); remap so each XCD owns a
@@ -74,148 +86,225 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
     tn = inner / gsz;
 }
 
-// One k-slab of op(A) (BM x BK) into registers.  !TA: A(i,k)=A[i + k*lda]
-// (i contiguous: lane -> i); TA: op(A)(i,k)=A[k + i*lda] (k contiguous: lane -> k).
-template <typename T, bool TA>
-__device__ __forceinline__ void load_a(const GemmParams<T>& p, i64 m0, i64 k0, int tid, T (&r)[EPT]) {
-    if (!TA) {
-        const int i = tid & (BM - 1), kk = tid >> 7;
-        const bool iv = (m0 + i) < p.m;
-        const T* base = p.A + (m0 + i) + (k0 + kk) * p.lda;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const bool v = iv && (k0 + kk + 2 * e) < p.k;
-            r[e] = v ? base[(i64)(2 * e) * p.lda] : T(0);
-        }
-    } else {
-        const int kk = tid & (BK - 1), i = tid >> 4;
-        const bool kv = (k0 + kk) < p.k;
-        const T* base = p.A + (k0 + kk) + (m0 + i) * p.lda;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const bool v = kv && (m0 + i + 16 * e) < p.m;
-            r[e] = v ? base[(i64)(16 * e) * p.lda] : T(0);
-        }
-    }
-}
-template <typename T, bool TA>
-__device__ __forceinline__ void store_a(T (*As)[LDP], int tid, const T (&r)[EPT]) {
-    if (!TA) {
-        const int i = tid & (BM - 1), kk = tid >> 7;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) As[kk + 2 * e][i] = r[e];
-    } else {
-        const int kk = tid & (BK - 1), i = tid >> 4;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) As[kk][i + 16 * e] = r[e];
-    }
-}
-// One k-slab of op(B) (BK x BN).  !TB: B(k,j)=B[k + j*ldb] (k contiguous);
-// TB: op(B)(k,j)=B[j + k*ldb] (j contiguous).
-template <typename T, bool TB>
-__device__ __forceinline__ void load_b(const GemmParams<T>& p, i64 n0, i64 k0, int tid, T (&r)[EPT]) {
-    if (TB) {
-        const int j = tid & (BN - 1), kk = tid >> 7;
-        const bool jv = (n0 + j) < p.n;
-        const T* base = p.B + (n0 + j) + (k0 + kk) * p.ldb;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const bool v = jv && (k0 + kk + 2 * e) < p.k;
-            r[e] = v ? base[(i64)(2 * e) * p.ldb] : T(0);
-        }
-    } else {
-        const int kk = tid & (BK - 1), j = tid >> 4;
-        const bool kv = (k0 + kk) < p.k;
-        const T* base = p.B + (k0 + kk) + (n0 + j) * p.ldb;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const bool v = kv && (n0 + j + 16 * e) < p.n;
-            r[e] = v ? base[(i64)(16 * e) * p.ldb] : T(0);
-        }
-    }
-}
-template <typename T, bool TB>
-__device__ __forceinline__ void store_b(T (*Bs)[LDP], int tid, const T (&r)[EPT]) {
-    if (TB) {
-        const int j = tid & (BN - 1), kk = tid >> 7;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) Bs[kk + 2 * e][j] = r[e];
-    } else {
-        const int kk = tid & (BK - 1), j = tid >> 4;
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) Bs[kk][j + 16 * e] = r[e];
-    }
-}
+// LDS image [k][r] of one operand slab (ROWS output rows x BK).
+template <typename T, int ROWS, bool RCONTIG>
+struct Img {
+    static constexpr int P = RCONTIG ? ROWS + 16 : ROWS + 17;
+    T d[BK][P];
+    __device__ __forceinline__ T& at(int r, int k) { return d[k][r]; }
+};
 
-template <typename T, bool TA, bool TB, bool BETA0>
-__global__ __launch_bounds__(NTHR, 2) void gemm_tile_kernel(GemmParams<T> p) {
+// Operand slab loader.  The operand is viewed as rows r (the output dimension:
+// i for A, j for B) by k.  RCONTIG: X(r,k) = X[r + k*ld]; else X(r,k) = X[k + r*ld].
+// Thread `tid` (of NTHR) owns element/pair p = tid + NTHR*q of the slab.
+template <typename T, int ROWS, bool RCONTIG, bool VEC, int NTHR>
+struct Slab {
+    using pair_t = typename Mfma<T>::pair_t;
+    static constexpr int STEP = VEC ? 2 : 1;
+    static constexpr int EPT = ROWS * BK / NTHR;  // elements per thread
+    static constexpr int NQ = EPT / STEP;          // loads per thread
+    static __device__ __forceinline__ int r_of(int tid, int q) {
+        const int p = tid + NTHR * q;
+        if (RCONTIG) return VEC ? 2 * (p % (ROWS / 2)) : p % ROWS;
+        return VEC ? p / (BK / 2) : p / BK;
+    }
+    static __device__ __forceinline__ int k_of(int tid, int q) {
+        const int p = tid + NTHR * q;
+        if (RCONTIG) return VEC ? p / (ROWS / 2) : p / ROWS;
+        return VEC ? 2 * (p % (BK / 2)) : p % BK;
+    }
+
+    // Generic path (any alignment / size): 64-bit clamped addresses.
+    static __device__ __forceinline__ void load_edge(const T* X, i64 ld, i64 rows, i64 kdim, i64 r0, i64 k0,
+                                                     int tid, T (&v)[EPT], uint32_t& ok) {
+        ok = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const i64 r = r0 + r_of(tid, q), k = k0 + k_of(tid, q);
+            ok |= (uint32_t)((r < rows) & (k < kdim)) << q;
+            if (VEC) {  // pairs never straddle the edge: even extent along the vector dimension
+                const i64 rc = r < rows ? r : rows - (RCONTIG ? 2 : 1);
+                const i64 kc = k < kdim ? k : kdim - (RCONTIG ? 1 : 2);
+                const pair_t x = *reinterpret_cast<const pair_t*>(RCONTIG ? X + rc + kc * ld : X + kc + rc * ld);
+                v[2 * q] = x[0];
+                v[2 * q + 1] = x[1];
+            } else {
+                const i64 rc = r < rows ? r : rows - 1, kc = k < kdim ? k : kdim - 1;
+                v[q] = RCONTIG ? X[rc + kc * ld] : X[kc + rc * ld];
+            }
+        }
+    }
+
+    // 32-bit path (VEC, ld < 2^24): every load is one 32-bit offset off the
+    // slab's uniform base; rows are clamped against the tile's uniform bound.
+    struct Off32 {
+        int rmax;  // last valid local row of this tile (uniform)
+    };
+    static __device__ __forceinline__ Off32 off32_init(int, i64 r0, i64 rows, uint32_t) {
+        const i64 rm = rows - r0 - (RCONTIG && VEC ? 2 : 1);
+        return Off32{rm > (1 << 30) ? (1 << 30) : (int)rm};
+    }
+    // sbase = X + slab origin (uniform); kleft = k extent left from the slab origin
+    static __device__ __forceinline__ void load32(const T* sbase, const Off32& st, int tid, uint32_t ld, int kleft,
+                                                  T (&v)[EPT], uint32_t& ok) {
+        ok = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int r = r_of(tid, q), kl = k_of(tid, q);
+            const int rc = min(r, st.rmax);
+            const int kc = min(kl, kleft - (RCONTIG ? 1 : 2));
+            ok |= (uint32_t)((r <= st.rmax) & (kl < kleft)) << q;
+            const uint32_t o = RCONTIG ? (uint32_t)rc + (uint32_t)kc * ld : (uint32_t)kc + (uint32_t)rc * ld;
+            const pair_t x = *reinterpret_cast<const pair_t*>(sbase + o);
+            v[2 * q] = x[0];
+            v[2 * q + 1] = x[1];
+        }
+    }
+
+    static __device__ __forceinline__ T sel(uint32_t ok, int q, T x) { return (ok >> q) & 1 ? x : T(0); }
+    static __device__ __forceinline__ void store(Img<T, ROWS, RCONTIG>& S, int tid, const T (&v)[EPT], uint32_t ok) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int r = r_of(tid, q), k = k_of(tid, q);
+            if (VEC) {
+                S.at(r, k) = sel(ok, q, v[2 * q]);
+                if (RCONTIG) S.at(r + 1, k) = sel(ok, q, v[2 * q + 1]);
+                else S.at(r, k + 1) = sel(ok, q, v[2 * q + 1]);
+            } else {
+                S.at(r, k) = sel(ok, q, v[q]);
+            }
+        }
+    }
+};
+
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int MINB_>
+struct TileCfg {
+    static constexpr int BM = BM_, BN = BN_, MINB = MINB_;
+    static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NTHR = 64 * WAVES_M_ * WAVES_N_;
+    static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;  // wave tile
+    static constexpr int WM = WTM / 16, WN = WTN / 16;            // MFMA tiles per wave
+    static constexpr int WAVES_PER_EU = MINB_ * WAVES_M_ * WAVES_N_ / 4;
+};
+using Tile128 = TileCfg<128, 128, 2, 2, 2>;   // 4 waves of 64x64, 2 per SIMD
+using Tile128w8 = TileCfg<128, 128, 4, 2, 2>; // 8 waves of 32x64, 4 per SIMD
+using Tile128w8n = TileCfg<128, 128, 2, 4, 2>;// 8 waves of 64x32, 4 per SIMD
+using Tile128w16 = TileCfg<128, 128, 4, 4, 2>;// 16 waves of 32x32, 8 per SIMD
+using Tile256 = TileCfg<256, 128, 2, 2, 1>;
+using Tile256w8 = TileCfg<256, 128, 4, 2, 1>;  // 8 waves of 64x64, 2 per SIMD, 1 block/CU
+
+template <typename T, typename CFG, bool TA, bool TB, bool BETA0, bool VEC, bool OFF32>
+__global__ __launch_bounds__(CFG::NTHR, CFG::WAVES_PER_EU) void gemm_tile_kernel(GemmParams<T> p) {
     using M = Mfma<T>;
     using acc_t = typename M::acc_t;
-    __shared__ T As[2][BK][LDP];
-    __shared__ T Bs[2][BK][LDP];
+    constexpr int BM = CFG::BM, BN = CFG::BN, WM = CFG::WM, WN = CFG::WN;
+    constexpr int WTM = CFG::WTM, WTN = CFG::WTN;
+    constexpr bool RA = !TA, RB = TB;  // op(A)(i,k): !TA -> A[i + k*lda]; op(B)(k,j): TB -> B[j + k*ldb]
+    using SA = Slab<T, BM, RA, VEC, CFG::NTHR>;
+    using SB = Slab<T, BN, RB, VEC, CFG::NTHR>;
+    __shared__ __attribute__((aligned(16))) Img<T, BM, RA> As[2];
+    __shared__ __attribute__((aligned(16))) Img<T, BN, RB> Bs[2];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / CFG::WAVES_N, wc = wave % CFG::WAVES_N;
     const int g = lane >> 4, c = lane & 15;
 
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
 
-    acc_t acc[4][4];
+    acc_t acc[WM][WN];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = acc_t{0, 0, 0, 0};
+        for (int b = 0; b < WN; ++b) acc[a][b] = acc_t{0, 0, 0, 0};
 
     const int nk = (int)((p.k + BK - 1) / BK);
-    T ra[EPT], rb[EPT];
+    typename SA::Off32 sta{};
+    typename SB::Off32 stb{};
+    if (OFF32) {
+        sta = SA::off32_init(tid, m0, p.m, (uint32_t)p.lda);
+        stb = SB::off32_init(tid, n0, p.n, (uint32_t)p.ldb);
+    }
+    T ra[SA::EPT], rb[SB::EPT];
+    uint32_t oka = 0, okb = 0;
+    auto load_slab = [&](int kt) {
+        const i64 k0 = (i64)kt * BK;
+        if (OFF32) {
+            const i64 kl = p.k - k0;
+            const int kleft = kl > (1 << 20) ? (1 << 20) : (int)kl;
+            SA::load32(p.A + (RA ? m0 + k0 * p.lda : m0 * p.lda + k0), sta, tid, (uint32_t)p.lda, kleft, ra, oka);
+            SB::load32(p.B + (RB ? n0 + k0 * p.ldb : n0 * p.ldb + k0), stb, tid, (uint32_t)p.ldb, kleft, rb, okb);
+        } else {
+            SA::load_edge(p.A, p.lda, p.m, p.k, m0, k0, tid, ra, oka);
+            SB::load_edge(p.B, p.ldb, p.n, p.k, n0, k0, tid, rb, okb);
+        }
+    };
     if (nk > 0) {
-        load_a<T, TA>(p, m0, 0, tid, ra);
-        load_b<T, TB>(p, n0, 0, tid, rb);
-        store_a<T, TA>(As[0], tid, ra);
-        store_b<T, TB>(Bs[0], tid, rb);
+        load_slab(0);
+        SA::store(As[0], tid, ra, oka);
+        SB::store(Bs[0], tid, rb, okb);
     }
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         const bool more = (kt + 1) < nk;
-        if (more) {  // issue next slab's loads early; they land during the MFMAs
-            load_a<T, TA>(p, m0, (i64)(kt + 1) * BK, tid, ra);
-            load_b<T, TB>(p, n0, (i64)(kt + 1) * BK, tid, rb);
-        }
+        if (more) load_slab(kt + 1);  // issued early; lands during the MFMAs
 #pragma unroll
         for (int s = 0; s < BK / 4; ++s) {
-            T a[4], b[4];
+            T a[WM], b[WN];
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi) a[mi] = As[cur][4 * s + g][wr * 64 + mi * 16 + c];
+            for (int mi = 0; mi < WM; ++mi) a[mi] = As[cur].at(wr * WTM + mi * 16 + c, 4 * s + g);
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[cur][4 * s + g][wc * 64 + ni * 16 + c];
+            for (int ni = 0; ni < WN; ++ni) b[ni] = Bs[cur].at(wc * WTN + ni * 16 + c, 4 * s + g);
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
+            for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = M::op(a[mi], b[ni], acc[mi][ni]);
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = M::op(a[mi], b[ni], acc[mi][ni]);
         }
         if (more) {
-            store_a<T, TA>(As[cur ^ 1], tid, ra);
-            store_b<T, TB>(Bs[cur ^ 1], tid, rb);
+            SA::store(As[cur ^ 1], tid, ra, oka);
+            SB::store(Bs[cur ^ 1], tid, rb, okb);
         }
         __syncthreads();
     }
 
     // Epilogue: C = alpha*acc + beta*C (beta == 0 never reads C: BLAS semantics).
+    // Interior tiles issue a row of C loads before their first use (no
+    // per-element branch), so the reads overlap instead of serialising.
+    const i64 ib = m0 + wr * WTM, jb = n0 + wc * WTN;
+    if (ib + WTM <= p.m && jb + WTN <= p.n) {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
+        for (int mi = 0; mi < WM; ++mi) {
+            T cv[WN][4];
+            if (!BETA0) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const i64 j = n0 + wc * 64 + ni * 16 + c;
+                for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        cv[ni][r] = p.C[(ib + mi * 16 + M::row(g, r)) + (jb + ni * 16 + c) * p.ldc];
+            }
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    T& o = p.C[(ib + mi * 16 + M::row(g, r)) + (jb + ni * 16 + c) * p.ldc];
+                    o = BETA0 ? p.alpha * acc[mi][ni][r] : p.alpha * acc[mi][ni][r] + p.beta * cv[ni][r];
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) {
+            const i64 j = jb + ni * 16 + c;
             if (j >= p.n) continue;
             T* ccol = p.C + j * p.ldc;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const i64 i = m0 + wr * 64 + mi * 16 + M::row(g, r);
+                const i64 i = ib + mi * 16 + M::row(g, r);
                 if (i < p.m) {
                     const T v = p.alpha * acc[mi][ni][r];
                     ccol[i] = BETA0 ? v : v + p.beta * ccol[i];
@@ -225,21 +314,57 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tile_kernel(GemmParams<T> p) {
     }
 }
 
-template <typename T, bool TA, bool TB>
-static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
+template <typename T, typename CFG, bool TA, bool TB, bool VEC, bool OFF32>
+static hipError_t launch_cfg(GemmParams<T> p, hipStream_t s) {
+    p.tiles_m = (int)((p.m + CFG::BM - 1) / CFG::BM);
+    p.tiles_n = (int)((p.n + CFG::BN - 1) / CFG::BN);
     const int nwg = p.tiles_m * p.tiles_n;
     if (p.beta == T(0))
-        hipLaunchKernelGGL((gemm_tile_kernel<T, TA, TB, true>), dim3(nwg), dim3(NTHR), 0, s, p);
+        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, true, VEC, OFF32>), dim3(nwg), dim3(CFG::NTHR), 0, s, p);
     else
-        hipLaunchKernelGGL((gemm_tile_kernel<T, TA, TB, false>), dim3(nwg), dim3(NTHR), 0, s, p);
+        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, false, VEC, OFF32>), dim3(nwg), dim3(CFG::NTHR), 0, s, p);
     return hipGetLastError();
+}
+
+// Tile configuration (measured on MI355X, tools/variants.sh, 16384^3 NN):
+//   f64: 128x128 with 8 waves of 32x64 (4 waves per SIMD)   66.1 TF vs 62.9 (4 waves), 62.8 (256x128)
+//   f32: 256x128 with 8 waves of 64x64 (1 block per CU)    127.5 TF vs 124.5 (128x128, 4 waves)
+// ELX_GEMM_TILE = 128 | 1288 | 1289 | 12816 | 256 | 2568 overrides (A/B measurements only).
+template <typename T>
+static int tile_choice() {
+    static const int forced = [] { const char* v = getenv("ELX_GEMM_TILE"); return v ? atoi(v) : 0; }();
+    if (forced) return forced;
+    return sizeof(T) == 8 ? 1288 : 2568;
+}
+
+template <typename T, bool TA, bool TB>
+static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
+    // 16-byte loads need 16-byte aligned bases, even leading dimensions and an
+    // even extent along each operand's unit-stride dimension.
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const bool a_even = TA ? (p.k % 2 == 0) : (p.m % 2 == 0);
+    const bool b_even = TB ? (p.n % 2 == 0) : (p.k % 2 == 0);
+    const bool vec = al(p.A) && al(p.B) && p.lda % 2 == 0 && p.ldb % 2 == 0 && a_even && b_even;
+    const bool off32 = vec && p.lda < (1 << 24) && p.ldb < (1 << 24);
+    const int tc = tile_choice<T>();
+    if (off32) {
+        switch (tc) {
+        case 256: return launch_cfg<T, Tile256, TA, TB, true, true>(p, s);
+        case 1288: return launch_cfg<T, Tile128w8, TA, TB, true, true>(p, s);
+        case 1289: return launch_cfg<T, Tile128w8n, TA, TB, true, true>(p, s);
+        case 12816: return launch_cfg<T, Tile128w16, TA, TB, true, true>(p, s);
+        case 2568: return launch_cfg<T, Tile256w8, TA, TB, true, true>(p, s);
+        default: return launch_cfg<T, Tile128, TA, TB, true, true>(p, s);
+        }
+    }
+    if (vec) return launch_cfg<T, Tile128, TA, TB, true, false>(p, s);
+    return launch_cfg<T, Tile128, TA, TB, false, false>(p, s);
 }
 
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s) {
-    GemmParams<T> p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc,
-                    (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN)};
+    GemmParams<T> p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0};
     if (ta) return tb ? launch_tn<T, true, true>(p, s) : launch_tn<T, true, false>(p, s);
     return tb ? launch_tn<T, false, true>(p, s) : launch_tn<T, false, false>(p, s);
 }
