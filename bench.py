@@ -47,8 +47,25 @@ def cpu_baseline(seconds_target: float = 15.0) -> dict:
         if t * 8 > seconds_target or s >= 4096:
             break
         s *= 2
-    return {"value": 2.0 * s ** 3 / t / 1e12, "unit": "TFLOP/s", "cores": 1, "kind": "port",
-            "sample": f"oracle C GEMM NN fp64 {s}x{s}x{s}, 1 thread, {t:.2f} s"}
+    reps, total = 1, t
+    while total < 10.0:  # about 10-30 s of CPU work in all
+        t0 = time.perf_counter()
+        oracle.gemm("N", "N", 0.5, A, B, -0.5, C)
+        total += time.perf_counter() - t0
+        reps += 1
+    return {"value": 2.0 * s ** 3 * reps / total / 1e12, "unit": "TFLOP/s", "cores": 1, "kind": "port",
+            "sample": f"oracle C GEMM NN fp64 {s}x{s}x{s} x{reps}, 1 thread, {total:.2f} s"}
+
+
+def measured_traffic(dtype: str, n: int, world: int):
+    """Per-launch HBM bytes of the GEMM kernel from the committed rocprofv3 PMC
+    passes of this same bench command (tools/collect_profiles.sh ->
+    profiles/traffic_index.json), or None when that configuration was not profiled."""
+    path = os.path.join(ROOT, "profiles", "traffic_index.json")
+    if not os.path.exists(path):
+        return None
+    ent = json.load(open(path)).get(f"{dtype}:{n}:{world}")
+    return ent["hbm_bytes_per_launch"] if ent else None
 
 
 def main():
@@ -164,7 +181,8 @@ def main():
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "traffic": None,
+            "traffic": measured_traffic(args.dtype, n, world),
+            "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
             "launches_timed": launches.value,
             "avg_launch_ms": round(avg_ms, 3),
             "flops_per_launch": flops_per_launch,
