@@ -87,6 +87,7 @@ _SIGS = {
     "elx_dm_set_local": (_i, [_vp, _vp, _i64]),
     "elx_dm_get_local": (_i, [_vp, _vp, _i64]),
     "elx_dm_view": (_i, [POINTER(c_void_p), _vp, _i64, _i64, _i64, _i64]),
+    "elx_dm_attach": (_i, [_vp, _i64, _i64, _i, _i, _vp, _i64, _i]),
     "elx_dm_copy": (_i, [_vp, _vp]),
     "elx_dm_transpose": (_i, [_vp, _vp]),
     "elx_dm_fill_hash": (_i, [_vp, c_uint64, _d, _d]),

@@ -249,6 +249,10 @@ int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld) { return Guard([&] { M(
 int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1) {
     return Guard([&] { *V = new elx_dm_s{DistMatrix::View(M(A), i0, i1, j0, j1)}; });
 }
+int elx_dm_attach(elx_dm_t A, int64_t height, int64_t width, int colAlign, int rowAlign, void* buffer,
+                  int64_t ldim, int root) {
+    return Guard([&] { M(A).Attach(height, width, colAlign, rowAlign, buffer, ldim, root); });
+}
 int elx_dm_copy(elx_dm_t B, elx_dm_t A) { return Guard([&] { Copy(M(A), M(B)); }); }
 int elx_dm_transpose(elx_dm_t A, elx_dm_t B) { return Guard([&] { Transpose(M(A), M(B)); }); }
 int elx_dm_fill_hash(elx_dm_t A, uint64_t seed, double center, double radius) {

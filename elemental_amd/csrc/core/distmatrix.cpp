@@ -173,6 +173,33 @@ void DistMatrix::Empty() {
     offset_ = 0;
 }
 
+// ElementalMatrix::Attach (src/core/DistMatrix/ElementMatrix.cpp:368-409): view
+// caller storage as this rank's local block; alignments become constrained.
+void DistMatrix::Attach(Int height, Int width, int colAlign, int rowAlign, void* buffer, Int ldim, int root) {
+    ELX_REQUIRE(height >= 0 && width >= 0, "negative dimensions");
+    ELX_REQUIRE(root >= 0 && root < G().Size(), "invalid root ", root);
+    const int cs = ColStride(), rs = RowStride();
+    ELX_REQUIRE(colAlign >= 0 && colAlign < cs, "invalid col alignment ", colAlign);
+    ELX_REQUIRE(rowAlign >= 0 && rowAlign < rs, "invalid row alignment ", rowAlign);
+    viewing_ = false;
+    Empty();
+    root_ = root;
+    h_ = height;
+    w_ = width;
+    calign_ = colAlign;
+    ralign_ = rowAlign;
+    cconstr_ = rconstr_ = true;
+    SetLocalSizes();
+    ELX_REQUIRE(ldim >= (lh_ > 0 ? lh_ : 1), "Leading dimension must be no less than height (", ldim, " < ",
+                lh_, ")");
+    ELX_REQUIRE(buffer != nullptr || lh_ * lw_ == 0, "null buffer for a nonempty local block");
+    ld_ = ldim;
+    offset_ = 0;
+    buf_ = std::make_shared<elx::Buffer>();
+    if (lh_ * lw_ > 0) buf_->Wrap(dev_, buffer, static_cast<size_t>(ldim * (lw_ - 1) + lh_) * ElemSize());
+    viewing_ = true;
+}
+
 void DistMatrix::AlignCols(int colAlign, bool constrain) {
     ELX_REQUIRE(colAlign >= 0 && colAlign < ColStride(), "invalid col alignment ", colAlign);
     ELX_REQUIRE(!(viewing_ && colAlign != calign_), "Tried to realign a view");

@@ -115,6 +115,8 @@ public:
     void Resize(Int height, Int width);
     void Empty();
 
+    // view caller storage (ElementalMatrix::Attach); the caller keeps ownership
+    void Attach(Int height, Int width, int colAlign, int rowAlign, void* buffer, Int ldim, int root);
     // V := A(i0:i1, j0:j1), sharing A's storage
     static std::shared_ptr<DistMatrix> View(const DistMatrix& A, Int i0, Int i1, Int j0, Int j1);
     // fresh matrix with the same grid/type/device

@@ -15,7 +15,7 @@
 //    their S extra copies of C.
 //  * communication panel (Blocksize(), default 128) and compute panel are
 //    decoupled: ComputePanel() consecutive columns of A / rows of B are moved
-//    per step (default 2048, whole k on a 1x1 grid where the "gathers" are
+//    per step (K/16 clamped to [2048, 8192], whole k on a 1x1 grid where the "gathers" are
 //    local views), so the fp64 update runs at k >= 2048 instead of k = 128 and
 //    C's HBM round trip per panel stays a few % of the MFMA time.  Only the
 //    summation order changes (normwise tolerance); data movement is bit-exact.
@@ -110,7 +110,10 @@ void Check(bool cond, const char* what) {
 Int EffectivePanel(const Grid& g, Int K) {
     const Int nb = std::max<Int>(1, g_blocksize);
     Int kc = g_compute_panel;
-    if (kc <= 0) kc = (g.Size() == 1) ? K : std::max<Int>(nb, 2048);
+    // automatic: C's HBM round trip per panel (16 B/element) against the
+    // panel's 2*kc FLOP/element stays ~2.5% of the MFMA time at kc = 4096
+    // (K = 65536 -> 16 panels); never below 2048, never above 8192
+    if (kc <= 0) kc = (g.Size() == 1) ? K : std::min<Int>(8192, std::max<Int>(2048, K / 16));
     kc = std::max<Int>(nb, (kc + nb - 1) / nb * nb);  // whole communication panels
     return std::max<Int>(1, kc);
 }

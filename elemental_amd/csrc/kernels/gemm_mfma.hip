@@ -6,13 +6,14 @@
 // (src/blas_like/level3/Gemm.cpp:163-186 LocalGemm -> Gemm_impl<GPU>).
 //
 // Design (MI355X-first):
-//  * One 256-thread workgroup per BM x BN output tile, 4 waves in a 2x2
-//    arrangement; each wave owns (BM/2) x (BN/2) as a grid of 16x16 MFMA
-//    accumulators (v_mfma_f64_16x16x4_f64 / v_mfma_f32_16x16x4_f32: one
-//    operand element per lane, so every orientation shares one LDS image [k][r]).
-//    Two shapes: 128x128 (2 workgroups per CU, 2 waves per SIMD) and 256x128
-//    (1 workgroup per CU, 1 wave per SIMD with 8x4 accumulators in the
-//    unified VGPR/AGPR file, fewer LDS reads and HBM bytes per MFMA).
+//  * One workgroup per BM x BN output tile, WAVES_M x WAVES_N waves; each wave
+//    owns a grid of 16x16 MFMA accumulators (v_mfma_f64_16x16x4_f64 /
+//    v_mfma_f32_16x16x4_f32: one operand element per lane, so every
+//    orientation shares one LDS image [k][r]).  Shipped shapes (measured,
+//    profiles/r01_tile_variants.log): f64 128x128 with 8 waves of 32x64
+//    (2 workgroups per CU = 4 waves per SIMD, enough to hide the LDS->MFMA
+//    latency of the 64-cycle f64 MFMA); f32 256x128 with 8 waves of 64x64
+//    (1 workgroup per CU, fewer LDS reads and HBM bytes per MFMA).
 //  * BK = 16 k-slab, double-buffered in LDS; the next slab's global loads are
 //    issued into registers before the current slab's MFMAs and written to the
 //    other LDS buffer after them (one barrier per slab).

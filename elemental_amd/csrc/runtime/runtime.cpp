@@ -96,6 +96,7 @@ void Buffer::Reset(Device d, size_t bytes, hipStream_t s) {
     dev_ = d;
     bytes_ = bytes;
     stream_ = s;
+    owned_ = true;
     if (bytes == 0) return;
     if (d == Device::GPU) {
         ptr_ = Runtime::Get().Alloc(bytes, s);
@@ -107,6 +108,12 @@ void Buffer::Reset(Device d, size_t bytes, hipStream_t s) {
 
 void Buffer::Release() {
     if (!ptr_) return;
+    if (!owned_) {
+        ptr_ = nullptr;
+        bytes_ = 0;
+        owned_ = true;
+        return;
+    }
     if (dev_ == Device::GPU) {
         try { Runtime::Get().Free(ptr_, stream_); } catch (...) {}
     } else {

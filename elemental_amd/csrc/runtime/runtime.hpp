@@ -53,12 +53,14 @@ public:
     Buffer& operator=(Buffer&& o) noexcept {
         if (this != &o) {
             Release();
-            dev_ = o.dev_; ptr_ = o.ptr_; bytes_ = o.bytes_; stream_ = o.stream_;
+            dev_ = o.dev_; ptr_ = o.ptr_; bytes_ = o.bytes_; stream_ = o.stream_; owned_ = o.owned_;
             o.ptr_ = nullptr; o.bytes_ = 0;
         }
         return *this;
     }
     void Reset(Device d, size_t bytes, hipStream_t s = nullptr);
+    // non-owning: caller storage (DistMatrix::Attach); never freed here
+    void Wrap(Device d, void* ptr, size_t bytes) { Release(); dev_ = d; ptr_ = ptr; bytes_ = bytes; owned_ = false; }
     void Release();
     void* data() const { return ptr_; }
     size_t bytes() const { return bytes_; }
@@ -69,6 +71,7 @@ private:
     void* ptr_ = nullptr;
     size_t bytes_ = 0;
     hipStream_t stream_ = nullptr;
+    bool owned_ = true;
 };
 
 }  // namespace elx

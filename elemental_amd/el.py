@@ -207,6 +207,14 @@ class DistMatrix:
         call("elx_dm_view", byref(h), self.h, r0, r1, c0, c1)
         return DistMatrix(self.grid, self.dtype, self.U, self.V, self.device, self.root, _handle=h, _parent=self)
 
+    def attach(self, height: int, width: int, col_align: int, row_align: int, ptr: int, ldim: int,
+               root: int = 0) -> "DistMatrix":
+        """View caller storage at address `ptr` (device pointer for GPU matrices)
+        as the local block (ElementalMatrix::Attach); the caller keeps it alive."""
+        call("elx_dm_attach", self.h, height, width, col_align, row_align, ptr, ldim, root)
+        self.root = root
+        return self
+
     def assign(self, other: "DistMatrix") -> "DistMatrix":
         """self = other  (DistMatrix::operator=, any distribution pair)."""
         call("elx_dm_copy", self.h, other.h)

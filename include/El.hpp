@@ -1,0 +1,290 @@
+// El.hpp — drop-in C++ surface of the El::Gemm path (header-only, over the C-ABI
+// in elemental_amd.h).  Names, signatures, enum ordinals and exception types
+// follow the reference (include/El/core/types.hpp, include/El/core/Grid.hpp,
+// include/El/core/DistMatrix/*, include/El/blas_like/level3.hpp:20-90,
+// include/El/blas_like/level1/*) so LBANN-style callers recompile against it:
+//
+//   El::Grid g(El::mpi::COMM_WORLD());            // or a communicator over RCCL / a host bridge
+//   El::DistMatrix<double, El::MC, El::MR, El::ELEMENT, El::Device::GPU> A(m, k, g), B(k, n, g), C(m, n, g);
+//   El::Gemm(El::NORMAL, El::NORMAL, 1.0, A, B, 0.0, C);
+//
+// Link with -lelemental_amd (elemental_amd/libelemental_amd.so).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "elemental_amd.h"
+
+namespace El {
+
+using Int = std::int64_t;
+
+// ---- enums (ordinals match the reference) --------------------------------
+enum Dist { MC = ELX_MC, MD = ELX_MD, MR = ELX_MR, VC = ELX_VC, VR = ELX_VR, STAR = ELX_STAR, CIRC = ELX_CIRC };
+enum DistWrap { ELEMENT = 0, BLOCK = 1 };
+enum Orientation { NORMAL = ELX_NORMAL, TRANSPOSE = ELX_TRANSPOSE, ADJOINT = ELX_ADJOINT };
+enum GridOrder { ROW_MAJOR = ELX_ROW_MAJOR, COLUMN_MAJOR = ELX_COLUMN_MAJOR };
+enum GemmAlgorithm {
+    GEMM_DEFAULT = ELX_GEMM_DEFAULT, GEMM_SUMMA_A_MS = ELX_GEMM_SUMMA_A_MS, GEMM_SUMMA_A = ELX_GEMM_SUMMA_A,
+    GEMM_SUMMA_B_MS = ELX_GEMM_SUMMA_B_MS, GEMM_SUMMA_B = ELX_GEMM_SUMMA_B, GEMM_SUMMA_C_MS = ELX_GEMM_SUMMA_C_MS,
+    GEMM_SUMMA_C = ELX_GEMM_SUMMA_C, GEMM_SUMMA_DOT = ELX_GEMM_SUMMA_DOT, GEMM_CANNON = ELX_GEMM_CANNON
+};
+enum class Device : unsigned char { CPU = ELX_DEVICE_CPU, GPU = ELX_DEVICE_GPU };
+
+// 16-bit element types: gpu_half_type (rocblas_half in the reference,
+// include/hydrogen/utils/HalfPrecision.hpp:123) and bfloat16 (new).
+struct gpu_half_type { std::uint16_t x; };
+struct bfloat16 { std::uint16_t x; };
+
+// ---- errors: the reference's exception types ------------------------------
+struct LogicError : std::logic_error { using std::logic_error::logic_error; };
+struct RuntimeError : std::runtime_error { using std::runtime_error::runtime_error; };
+struct UnsupportedError : LogicError { using LogicError::LogicError; };
+namespace hydrogen_errors {
+struct GPUError : std::runtime_error { using std::runtime_error::runtime_error; };  // hydrogen::GPUError
+}
+
+namespace detail {
+inline void Check(int rc) {
+    if (rc == ELX_OK) return;
+    const std::string msg = elx_last_error();
+    switch (rc) {
+    case ELX_ERR_LOGIC: throw LogicError(msg);
+    case ELX_ERR_UNSUPPORTED: throw UnsupportedError(msg);
+    case ELX_ERR_HIP:
+    case ELX_ERR_NO_DEVICE: throw hydrogen_errors::GPUError(msg);
+    default: throw RuntimeError(msg);
+    }
+}
+template <typename T> struct TypeCode;
+template <> struct TypeCode<float> { static constexpr int value = ELX_F32; };
+template <> struct TypeCode<double> { static constexpr int value = ELX_F64; };
+template <> struct TypeCode<gpu_half_type> { static constexpr int value = ELX_F16; };
+template <> struct TypeCode<bfloat16> { static constexpr int value = ELX_BF16; };
+template <typename T> double ToDouble(T x) { return static_cast<double>(x); }
+}  // namespace detail
+
+// ---- Range / views ---------------------------------------------------------
+struct Range { Int beg, end; };
+inline Range IR(Int beg, Int end) { return Range{beg, end}; }
+inline Range IR(Int i) { return Range{i, i + 1}; }
+struct AllRange {};
+static constexpr AllRange ALL{};
+
+// ---- communicator ----------------------------------------------------------
+namespace mpi {
+class Comm {
+public:
+    Comm() = default;
+    explicit Comm(elx_comm_t c) : c_(c, [](elx_comm_s* p) { if (p) elx_comm_destroy(p); }) {}
+    // size-1 communicator (also what Grid() uses by default)
+    static Comm Self() {
+        elx_comm_t c = nullptr;
+        detail::Check(elx_comm_init_host(&c, 0, 1, nullptr, nullptr, nullptr));
+        return Comm(c);
+    }
+    // RCCL world: every rank passes the same 128-byte id (elx_comm_unique_id on one rank)
+    static Comm RCCL(int rank, int size, const unsigned char id[128]) {
+        elx_comm_t c = nullptr;
+        detail::Check(elx_comm_init_rccl(&c, rank, size, id));
+        return Comm(c);
+    }
+    int Rank() const { int r = 0; detail::Check(elx_comm_rank(c_.get(), &r)); return r; }
+    int Size() const { int s = 1; detail::Check(elx_comm_size(c_.get(), &s)); return s; }
+    elx_comm_t Handle() const { return c_.get(); }
+private:
+    std::shared_ptr<elx_comm_s> c_;
+};
+inline Comm COMM_SELF() { return Comm::Self(); }
+}  // namespace mpi
+
+// ---- El::Grid (src/core/Grid.cpp) --------------------------------------------
+class Grid {
+public:
+    explicit Grid(const mpi::Comm& comm = mpi::Comm::Self(), int height = 0, GridOrder order = COLUMN_MAJOR)
+        : comm_(comm) {
+        elx_grid_t g = nullptr;
+        detail::Check(elx_grid_create(&g, comm.Handle(), height, order));
+        g_.reset(g, [](elx_grid_s* p) { if (p) elx_grid_destroy(p); });
+        detail::Check(elx_grid_info(g, info_));
+    }
+    Grid(const mpi::Comm& comm, GridOrder order) : Grid(comm, 0, order) {}
+    static int DefaultHeight(int size) { return elx_grid_default_height(size); }
+    int Height() const { return info_[0]; }
+    int Width() const { return info_[1]; }
+    int Size() const { return info_[2]; }
+    int Rank() const { return info_[3]; }
+    int MCRank() const { return info_[4]; }
+    int MRRank() const { return info_[5]; }
+    int VCRank() const { return info_[6]; }
+    int VRRank() const { return info_[7]; }
+    elx_grid_t Handle() const { return g_.get(); }
+private:
+    mpi::Comm comm_;
+    std::shared_ptr<elx_grid_s> g_;
+    int info_[8] = {};
+};
+
+// ---- DistMatrix ----------------------------------------------------------------
+template <typename T>
+class AbstractDistMatrix {
+public:
+    virtual ~AbstractDistMatrix() = default;
+    Int Height() const { return Info(0); }
+    Int Width() const { return Info(1); }
+    Int LocalHeight() const { return Info(2); }
+    Int LocalWidth() const { return Info(3); }
+    Int LDim() const { return Info(4); }
+    int ColAlign() const { return (int)Info(5); }
+    int RowAlign() const { return (int)Info(6); }
+    int ColShift() const { return (int)Info(7); }
+    int RowShift() const { return (int)Info(8); }
+    int ColStride() const { return (int)Info(9); }
+    int RowStride() const { return (int)Info(10); }
+    bool Participating() const { return Info(11) != 0; }
+    bool Viewing() const { return Info(12) != 0; }
+    Dist ColDist() const { return cd_; }
+    Dist RowDist() const { return rd_; }
+    Device GetLocalDevice() const { return dev_; }
+    const El::Grid& Grid() const { return *grid_; }
+    Int GlobalRow(Int iLoc) const { return ColShift() + iLoc * ColStride(); }
+    Int GlobalCol(Int jLoc) const { return RowShift() + jLoc * RowStride(); }
+
+    void Resize(Int height, Int width) { detail::Check(elx_dm_resize(h(), height, width)); }
+    void Align(int colAlign, int rowAlign, bool constrain = true) {
+        detail::Check(elx_dm_align(h(), colAlign, rowAlign, constrain));
+    }
+    void AlignWith(const AbstractDistMatrix<T>& other, bool constrain = true) {
+        detail::Check(elx_dm_align_with(h(), other.h(), constrain));
+    }
+    // ElementalMatrix::Attach: view caller storage as this rank's local block
+    void Attach(Int height, Int width, const El::Grid& /*grid: must be this matrix's*/, int colAlign, int rowAlign,
+                T* buffer, Int ldim, int root = 0) {
+        detail::Check(elx_dm_attach(h(), height, width, colAlign, rowAlign, buffer, ldim, root));
+    }
+    T* Buffer() { void* p = nullptr; detail::Check(elx_dm_buffer(h(), &p)); return static_cast<T*>(p); }
+    const T* LockedBuffer() const { void* p = nullptr; detail::Check(elx_dm_buffer(h(), &p)); return static_cast<const T*>(p); }
+    // host <-> local block (column-major, leading dimension ld)
+    void SetLocalBlock(const T* host, Int ld) { detail::Check(elx_dm_set_local(h(), host, ld)); }
+    void GetLocalBlock(T* host, Int ld) const { detail::Check(elx_dm_get_local(h(), host, ld)); }
+    void Synchronize() const { detail::Check(elx_dm_synchronize(h())); }
+    elx_dm_t h() const { return dm_.get(); }
+
+protected:
+    AbstractDistMatrix(const El::Grid& g, Dist cd, Dist rd, Device dev, int root)
+        : grid_(&g), cd_(cd), rd_(rd), dev_(dev) {
+        elx_dm_t m = nullptr;
+        detail::Check(elx_dm_create(&m, g.Handle(), detail::TypeCode<T>::value, cd, rd,
+                                    static_cast<int>(dev), root));
+        dm_.reset(m, [](elx_dm_s* p) { if (p) elx_dm_destroy(p); });
+    }
+    AbstractDistMatrix(const El::Grid& g, Dist cd, Dist rd, Device dev, elx_dm_t view)
+        : grid_(&g), cd_(cd), rd_(rd), dev_(dev), dm_(view, [](elx_dm_s* p) { if (p) elx_dm_destroy(p); }) {}
+    Int Info(int i) const {
+        Int v[13];
+        detail::Check(elx_dm_info(h(), v));
+        return v[i];
+    }
+    const El::Grid* grid_;
+    Dist cd_, rd_;
+    Device dev_;
+    std::shared_ptr<elx_dm_s> dm_;
+};
+
+template <typename T, Dist U = MC, Dist V = MR, DistWrap W = ELEMENT, Device D = Device::CPU>
+class DistMatrix : public AbstractDistMatrix<T> {
+    static_assert(W == ELEMENT, "BLOCK distributions are outside the El::Gemm path");
+public:
+    explicit DistMatrix(const El::Grid& g, int root = 0) : AbstractDistMatrix<T>(g, U, V, D, root) {}
+    DistMatrix(Int height, Int width, const El::Grid& g, int root = 0) : DistMatrix(g, root) {
+        this->Resize(height, width);
+    }
+    // cross-distribution / cross-device copy construction (DistMatrix(const DistMatrix<T,U2,V2,...>&))
+    template <Dist U2, Dist V2, Device D2>
+    explicit DistMatrix(const DistMatrix<T, U2, V2, ELEMENT, D2>& A) : DistMatrix(A.Grid()) { *this = A; }
+    DistMatrix(const DistMatrix& A) : DistMatrix(A.Grid()) { *this = A; }
+    DistMatrix& operator=(const DistMatrix& A) {
+        if (this != &A) detail::Check(elx_dm_copy(this->h(), A.h()));
+        return *this;
+    }
+    // operator= : the redistribution table (bit-exact)
+    DistMatrix& operator=(const AbstractDistMatrix<T>& A) {
+        detail::Check(elx_dm_copy(this->h(), A.h()));
+        return *this;
+    }
+    // A(IR(i0,i1), IR(j0,j1)) views
+    DistMatrix operator()(Range rows, Range cols) const { return View(rows.beg, rows.end, cols.beg, cols.end); }
+    DistMatrix operator()(AllRange, Range cols) const { return View(0, this->Height(), cols.beg, cols.end); }
+    DistMatrix operator()(Range rows, AllRange) const { return View(rows.beg, rows.end, 0, this->Width()); }
+
+private:
+    DistMatrix(const El::Grid& g, elx_dm_t view) : AbstractDistMatrix<T>(g, U, V, D, view) {}
+    DistMatrix View(Int i0, Int i1, Int j0, Int j1) const {
+        elx_dm_t v = nullptr;
+        detail::Check(elx_dm_view(&v, this->h(), i0, i1, j0, j1));
+        return DistMatrix(this->Grid(), v);
+    }
+};
+
+// ---- level 3 (include/El/blas_like/level3.hpp:37-90) ----------------------------
+template <typename T>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
+          const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C, GemmAlgorithm alg = GEMM_DEFAULT) {
+    detail::Check(elx_gemm(orientA, orientB, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h(), alg));
+}
+// beta-less form: C is resized to op(A) op(B) and overwritten (Gemm.cpp:304-316)
+template <typename T>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
+          const AbstractDistMatrix<T>& B, AbstractDistMatrix<T>& C, GemmAlgorithm alg = GEMM_DEFAULT) {
+    const Int m = orientA == NORMAL ? A.Height() : A.Width();
+    const Int n = orientB == NORMAL ? B.Width() : B.Height();
+    C.Resize(m, n);
+    detail::Check(elx_gemm(orientA, orientB, detail::ToDouble(alpha), A.h(), B.h(), 0.0, C.h(), alg));
+}
+template <typename T>
+void LocalGemm(Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
+               const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
+    detail::Check(elx_local_gemm(orientA, orientB, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h()));
+}
+
+// ---- level 1 front doors ------------------------------------------------------------
+template <typename T> void Copy(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) { detail::Check(elx_dm_copy(B.h(), A.h())); }
+template <typename T> void Transpose(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, bool /*conjugate*/ = false) {
+    detail::Check(elx_dm_transpose(A.h(), B.h()));
+}
+template <typename T, typename S> void Axpy(S alpha, const AbstractDistMatrix<T>& X, AbstractDistMatrix<T>& Y) {
+    detail::Check(elx_dm_axpy(static_cast<double>(alpha), X.h(), Y.h()));
+}
+template <typename T, typename S> void Scale(S alpha, AbstractDistMatrix<T>& A) {
+    detail::Check(elx_dm_scale(static_cast<double>(alpha), A.h()));
+}
+template <typename T> void Zero(AbstractDistMatrix<T>& A) { detail::Check(elx_dm_zero(A.h())); }
+template <typename T> void Hadamard(const AbstractDistMatrix<T>& A, const AbstractDistMatrix<T>& B, AbstractDistMatrix<T>& C) {
+    detail::Check(elx_dm_hadamard(A.h(), B.h(), C.h()));
+}
+enum class EntrywiseFn { IDENTITY = ELX_MAP_IDENTITY, NEGATE = ELX_MAP_NEGATE, ABS = ELX_MAP_ABS, SQUARE = ELX_MAP_SQUARE,
+                         SQRT = ELX_MAP_SQRT, EXP = ELX_MAP_EXP, LOG = ELX_MAP_LOG, RELU = ELX_MAP_RELU,
+                         SIGMOID = ELX_MAP_SIGMOID, RECIPROCAL = ELX_MAP_RECIP, TANH = ELX_MAP_TANH };
+template <typename T> void EntrywiseMap(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, EntrywiseFn f) {
+    detail::Check(elx_dm_entrywise_map(static_cast<int>(f), A.h(), B.h()));
+}
+template <typename T, typename S> void AxpyContract(S alpha, const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) {
+    detail::Check(elx_dm_axpy_contract(static_cast<double>(alpha), A.h(), B.h()));
+}
+// grid-independent synthetic fill (stands in for Uniform(A, m, n, center, radius) in benchmarks)
+template <typename T> void HashFill(AbstractDistMatrix<T>& A, std::uint64_t seed, double center, double radius) {
+    detail::Check(elx_dm_fill_hash(A.h(), seed, center, radius));
+}
+
+// ---- environment ------------------------------------------------------------------
+inline void SetBlocksize(Int nb) { detail::Check(elx_set_blocksize(nb)); }
+inline Int Blocksize() { return elx_blocksize(); }
+inline void Initialize() {}
+inline void Initialize(int&, char**&) {}
+inline void Finalize() {}
+
+}  // namespace El

@@ -64,7 +64,7 @@ extern "C" {
 #define ELX_F16  2   /* gpu_half_type (rocblas_half), include/hydrogen/utils/HalfPrecision.hpp:123 */
 #define ELX_BF16 3   /* new: no reference counterpart */
 /* entrywise functors for elx_entrywise_map (the C-ABI cannot carry a device
- * lambda; the C++ header El/EntrywiseMap.hpp keeps the templated form)      */
+ * lambda; include/El.hpp maps them to El::EntrywiseFn)      */
 #define ELX_MAP_IDENTITY 0
 #define ELX_MAP_NEGATE   1
 #define ELX_MAP_ABS      2
@@ -217,6 +217,11 @@ int elx_dm_set_local(elx_dm_t A, const void* host, int64_t ld);
 int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld);
 /* V := A(i0:i1, j0:j1) (a view, El::View / A(IR,IR)) */
 int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1);
+/* A views caller storage as its local block: ElementalMatrix::Attach
+ * (src/core/DistMatrix/ElementMatrix.cpp:368-409).  Alignments become
+ * constrained, the caller keeps ownership, ldim >= max(localHeight, 1). */
+int elx_dm_attach(elx_dm_t A, int64_t height, int64_t width, int colAlign, int rowAlign,
+                  void* buffer, int64_t ldim, int root);
 /* B := A  (DistMatrix::operator=, the redistribution dispatch table,
  * src/core/DistMatrix/ElementMatrix/{MC_MR,MC_STAR,...}.cpp); bit-exact */
 int elx_dm_copy(elx_dm_t B, elx_dm_t A);

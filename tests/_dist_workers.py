@@ -23,6 +23,13 @@ def init(rank: int, world: int, port: int):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     from elemental_amd import el
+    if os.environ.get("ELX_TEST_BACKEND") == "rccl":
+        # one GPU per rank, data over RCCL; gloo only carries the unique id
+        from elemental_amd import _lib as L
+        L.call("elx_set_device", rank)
+        obj = [el.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return el, el.Comm.rccl(rank, world, obj[0])
     from elemental_amd.torch_bridge import GlooBridge
     bridge = GlooBridge()
     return el, el.Comm.host(bridge)

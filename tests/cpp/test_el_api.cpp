@@ -1,0 +1,160 @@
+// Compiled check of the drop-in C++ surface (include/El.hpp) on Device::CPU
+// matrices over a 1x1 grid: it must compile the way reference callers write
+// El::Gemm code (tests/blas_like/Gemm.cpp:20-140 shape) and give the same
+// answers as a plain triple loop.  Built and run by tests/test_capi_cpu.py.
+#include <El.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+static int failures = 0;
+#define EXPECT(cond)                                                        \
+    do {                                                                    \
+        if (!(cond)) {                                                      \
+            std::fprintf(stderr, "%s:%d: EXPECT(%s) failed\n", __FILE__, __LINE__, #cond); \
+            ++failures;                                                     \
+        }                                                                   \
+    } while (0)
+
+template <typename T, El::Dist U, El::Dist V>
+static std::vector<T> Local(const El::DistMatrix<T, U, V>& A) {
+    std::vector<T> h(std::max<El::Int>(A.LocalHeight() * A.LocalWidth(), 1));
+    A.GetLocalBlock(h.data(), std::max<El::Int>(A.LocalHeight(), 1));
+    return h;
+}
+
+int main() {
+    using El::Int;
+    El::Initialize();
+    El::Grid g;  // 1x1 over COMM_SELF
+    EXPECT(g.Height() == 1 && g.Width() == 1 && g.Size() == 1);
+    EXPECT(El::Grid::DefaultHeight(8) == 2 && El::Grid::DefaultHeight(4) == 2 && El::Grid::DefaultHeight(2) == 1);
+
+    const Int m = 37, n = 29, k = 41;
+    El::DistMatrix<double> A(m, k, g), B(k, n, g), C(m, n, g);
+    El::HashFill(A, 11, 0.0, 1.0);
+    El::HashFill(B, 12, 0.0, 1.0);
+    El::HashFill(C, 13, 0.0, 1.0);
+    EXPECT(A.Height() == m && A.Width() == k && A.LocalHeight() == m && A.LDim() >= m);
+    EXPECT(A.ColDist() == El::MC && A.RowDist() == El::MR && A.GetLocalDevice() == El::Device::CPU);
+    const auto a = Local(A), b = Local(B), c0 = Local(C);
+
+    // C := 0.5 A B - 0.25 C
+    El::Gemm(El::NORMAL, El::NORMAL, 0.5, A, B, -0.25, C);
+    auto c = Local(C);
+    double err = 0, ref = 0;
+    for (Int j = 0; j < n; ++j)
+        for (Int i = 0; i < m; ++i) {
+            double s = 0;
+            for (Int l = 0; l < k; ++l) s += a[i + l * m] * b[l + j * k];
+            const double want = 0.5 * s - 0.25 * c0[i + j * m];
+            err = std::max(err, std::fabs(c[i + j * m] - want));
+            ref = std::max(ref, std::fabs(want));
+        }
+    EXPECT(err <= 1e-13 * (ref + 1));
+
+    // beta-less form resizes C; transpose orientation: D := A^T A  (k x k)
+    El::DistMatrix<double> D(g);
+    El::Gemm(El::TRANSPOSE, El::NORMAL, 1.0, A, A, D, El::GEMM_SUMMA_C);
+    EXPECT(D.Height() == k && D.Width() == k);
+    auto d = Local(D);
+    err = 0;
+    for (Int j = 0; j < k; ++j)
+        for (Int i = 0; i < k; ++i) {
+            double s = 0;
+            for (Int l = 0; l < m; ++l) s += a[l + i * m] * a[l + j * m];
+            err = std::max(err, std::fabs(d[i + j * k] - s));
+        }
+    EXPECT(err <= 1e-12);
+
+    // redistribution + transpose + view are bit-exact
+    El::DistMatrix<double, El::STAR, El::STAR> S(A);
+    EXPECT(Local(S) == a);
+    El::DistMatrix<double, El::VR, El::STAR> R(g);
+    R = A;
+    EXPECT(Local(R) == a);
+    El::DistMatrix<double> T(g);
+    El::Transpose(A, T);
+    auto t = Local(T);
+    bool tok = T.Height() == k && T.Width() == m;
+    for (Int j = 0; j < m && tok; ++j)
+        for (Int i = 0; i < k; ++i) tok &= t[i + j * k] == a[j + i * m];
+    EXPECT(tok);
+    auto Av = A(El::IR(3, 10), El::IR(5, 9));
+    EXPECT(Av.Height() == 7 && Av.Width() == 4 && Av.Viewing());
+    El::DistMatrix<double> W(Av);
+    auto w = Local(W);
+    bool vok = true;
+    for (Int j = 0; j < 4; ++j)
+        for (Int i = 0; i < 7; ++i) vok &= w[i + j * 7] == a[(3 + i) + (5 + j) * m];
+    EXPECT(vok);
+
+    // level-1 front doors
+    El::DistMatrix<double> Y(S);
+    El::Axpy(2.0, A, Y);   // Y = 3A
+    El::Scale(0.5, Y);     // Y = 1.5A
+    auto y = Local(Y);
+    bool aok = true;
+    for (size_t i = 0; i < a.size(); ++i) aok &= std::fabs(y[i] - 1.5 * a[i]) <= 1e-15 * std::fabs(a[i]) + 1e-300;
+    EXPECT(aok);
+    El::EntrywiseMap(A, Y, El::EntrywiseFn::SQUARE);
+    El::DistMatrix<double> H(g);
+    H.Resize(m, k);
+    El::Hadamard(A, A, H);
+    EXPECT(Local(H) == Local(Y));
+    El::Zero(H);
+    for (double v : Local(H)) EXPECT(v == 0.0);
+
+    // float path
+    El::DistMatrix<float> Af(8, 8, g), Bf(8, 8, g), Cf(8, 8, g);
+    El::HashFill(Af, 1, 0.0, 1.0);
+    El::HashFill(Bf, 2, 0.0, 1.0);
+    El::Gemm(El::NORMAL, El::TRANSPOSE, 1.0f, Af, Bf, 0.0f, Cf);
+    auto af = Local(Af), bf = Local(Bf), cf = Local(Cf);
+    float ferr = 0;
+    for (int j = 0; j < 8; ++j)
+        for (int i = 0; i < 8; ++i) {
+            float s = 0;
+            for (int l = 0; l < 8; ++l) s += af[i + l * 8] * bf[j + l * 8];
+            ferr = std::max(ferr, std::fabs(cf[i + j * 8] - s));
+        }
+    EXPECT(ferr <= 1e-5f);
+
+    // error mapping: nonconformal Gemm is a LogicError, as Gemm.cpp:279-283
+    bool threw = false;
+    try {
+        El::Gemm(El::NORMAL, El::NORMAL, 1.0, A, A, 0.0, C);
+    } catch (const El::LogicError&) {
+        threw = true;
+    }
+    EXPECT(threw);
+
+    // Attach: caller storage with ldim > height, computed into in place
+    std::vector<double> cbuf((m + 2) * n, 9.0);
+    El::DistMatrix<double> Ca(g);
+    Ca.Attach(m, n, g, 0, 0, cbuf.data(), m + 2);
+    EXPECT(Ca.Viewing() && Ca.LDim() == m + 2);
+    El::Gemm(El::NORMAL, El::NORMAL, 0.5, A, B, 0.0, Ca);
+    bool tok2 = true;
+    for (Int j = 0; j < n; ++j) {
+        for (Int i = 0; i < m; ++i) {
+            double s = 0;
+            for (Int l = 0; l < k; ++l) s += a[i + l * m] * b[l + j * k];
+            tok2 &= std::fabs(cbuf[i + j * (m + 2)] - 0.5 * s) <= 1e-13;
+        }
+        tok2 &= cbuf[m + j * (m + 2)] == 9.0 && cbuf[m + 1 + j * (m + 2)] == 9.0;
+    }
+    EXPECT(tok2);
+
+    El::SetBlocksize(64);
+    EXPECT(El::Blocksize() == 64);
+    El::SetBlocksize(128);
+    El::Finalize();
+    if (failures) {
+        std::fprintf(stderr, "%d failures\n", failures);
+        return 1;
+    }
+    std::printf("El.hpp API test OK\n");
+    return 0;
+}

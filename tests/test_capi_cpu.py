@@ -1,0 +1,130 @@
+"""The C-ABI boundary on CPU: the library loads, exports every symbol the
+headers declare, maps errors to the reference's exception types, fails loudly
+without a device, and the drop-in C++ header compiles and runs (Device::CPU
+matrices, 1x1 grid).  No GPU compute here."""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from elemental_amd import _lib as L
+from elemental_amd import el
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "elemental_amd.h")
+
+
+def test_every_declared_symbol_is_exported():
+    names = L.declared_symbols(HEADER)
+    assert len(names) >= 70
+    lib = L.lib()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and nm agrees that they are real dynamic exports with C linkage
+    if shutil.which("nm"):
+        out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+        exported = set(re.findall(r"\sT\s(elx_\w+)$", out, re.M))
+        assert set(names) <= exported, sorted(set(names) - exported)
+
+
+def test_python_signatures_cover_header():
+    assert set(L.declared_symbols(HEADER)) == set(L._SIGS), set(L.declared_symbols(HEADER)) ^ set(L._SIGS)
+
+
+def test_enum_ordinals_match_reference():
+    text = open(HEADER).read()
+    vals = dict((k, int(v)) for k, v in re.findall(r"#define (ELX_\w+)\s+(\d+)", text))
+    # El::Dist (include/El/core/types.hpp), El::Orientation, El::GemmAlgorithm (level3.hpp:22-35)
+    assert [vals[f"ELX_{d}"] for d in ("MC", "MD", "MR", "VC", "VR", "STAR", "CIRC")] == list(range(7))
+    assert [vals[f"ELX_{o}"] for o in ("NORMAL", "TRANSPOSE", "ADJOINT")] == [0, 1, 2]
+    algs = ["DEFAULT", "SUMMA_A_MS", "SUMMA_A", "SUMMA_B_MS", "SUMMA_B", "SUMMA_C_MS", "SUMMA_C", "SUMMA_DOT",
+            "CANNON"]
+    assert [vals[f"ELX_GEMM_{a}"] for a in algs] == list(range(9))
+    assert (el.MC, el.MR, el.STAR, el.CIRC) == (0, 2, 5, 6)
+
+
+def test_error_mapping_and_messages():
+    g = el.Grid()
+    A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=4, width=3)
+    B = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=4, width=3)
+    C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=4, width=3)
+    with pytest.raises(L.LogicError, match="onformal|dimension|match"):
+        el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, B, 0.0, C)
+    with pytest.raises(L.LogicError):
+        L.call("elx_dm_create", L.ctypes.byref(L.ctypes.c_void_p()), g.h, el.F64, el.MD, el.STAR, el.CPU, 0)
+    with pytest.raises(L.UnsupportedError):
+        el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=3, width=3),
+                0.0, C, alg=el.GEMM_CANNON)
+
+
+def test_gpu_matrix_without_device_fails_loudly():
+    if el.device_count() > 0:
+        pytest.skip("a device is visible")
+    g = el.Grid()
+    with pytest.raises(L.ElxError):
+        el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=8, width=8)
+    with pytest.raises(L.ElxError):
+        L.call("elx_gemm_f64", 0, 0, 1, 1, 1, 1.0, None, 1, None, 1, 0.0, None, 1, None)
+
+
+def test_cpu_matrices_local_gemm_and_redistribution():
+    g = el.Grid()
+    import oracle
+    Ah, Bh, Ch = oracle.hash_matrix(17, 9, 1), oracle.hash_matrix(9, 6, 2), oracle.hash_matrix(17, 6, 3)
+    A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=17, width=9)
+    B = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=9, width=6)
+    C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=17, width=6)
+    A.set_local(Ah), B.set_local(Bh), C.set_local(Ch)
+    el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
+    want = oracle.gemm("N", "N", 0.5, Ah, Bh, -0.5, Ch)
+    assert oracle.parity_ratio(C.get_local(), want, Ah, Bh, 9, np.finfo(float).eps) <= 10
+    S = el.DistMatrix(g, el.F64, el.STAR, el.VC, el.CPU)
+    S.assign(A)
+    assert np.array_equal(S.get_local(), Ah)
+
+
+def test_cpp_dropin_header_compiles_and_runs(tmp_path):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = tmp_path / "test_el_api"
+    libdir = os.path.dirname(L.LIB_PATH)
+    subprocess.check_call([gxx, "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "test_el_api.cpp"), "-o", str(exe), "-L", libdir,
+                           "-lelemental_amd", f"-Wl,-rpath,{libdir}"])
+    res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert "OK" in res.stdout
+
+
+def test_c_header_is_plain_c():
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no gcc")
+    # the boundary header must compile as C99 (no C++ types leak into signatures)
+    subprocess.check_call([gcc, "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", HEADER])
+
+
+def test_attach_caller_storage():
+    """ElementalMatrix::Attach: the library computes straight into caller memory."""
+    import oracle
+    g = el.Grid()
+    m, n, k = 11, 7, 5
+    Ah = oracle.hash_matrix(m, k, 1)
+    Bh = oracle.hash_matrix(k, n, 2)
+    Cpad = np.asfortranarray(np.full((m + 3, n), 7.0))   # ldim = m + 3, padding rows untouched
+    A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU).attach(m, k, 0, 0, Ah.ctypes.data, m)
+    B = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU).attach(k, n, 0, 0, Bh.ctypes.data, k)
+    C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU).attach(m, n, 0, 0, Cpad.ctypes.data, m + 3)
+    assert C.info()["ldim"] == m + 3 and C.info()["viewing"]
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, B, 0.0, C)
+    want = oracle.gemm("N", "N", 1.0, Ah, Bh, 0.0, np.zeros((m, n), order="F"))
+    assert oracle.parity_ratio(Cpad[:m], want, Ah, Bh, k, np.finfo(float).eps) <= 10
+    assert (Cpad[m:] == 7.0).all()
+    with pytest.raises(L.LogicError):
+        C.Resize(3, 3)
+    with pytest.raises(L.LogicError):
+        el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU).attach(m, n, 0, 0, Cpad.ctypes.data, m - 1)

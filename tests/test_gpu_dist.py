@@ -89,3 +89,51 @@ def test_gpu_gemm_associativity_large(oA, oB):
     E = Y - Cf @ X
     res = np.linalg.norm(E) / np.linalg.norm(Y)
     assert res < 1e-13, res  # reference measured 2.3e-16 at 4096
+
+
+def _rccl_spawn(fn, world, *args):
+    import os
+    os.environ["ELX_TEST_BACKEND"] = "rccl"
+    try:
+        _spawn(fn, world, *args)
+    finally:
+        os.environ.pop("ELX_TEST_BACKEND", None)
+
+
+def test_gpu_rccl_single_rank_redistribution_and_summa():
+    """The RCCL backend end to end at world size 1 (init, the four grid
+    splits, the self-copy paths) - the only RCCL shape a 1-GPU box can run."""
+    _rccl_spawn(W.redist_worker, 1, 1, el.GPU, el.F64, 13, 11, 77)
+    _rccl_spawn(W.gemm_worker, 1, 1, el.GPU, el.F64, [(45, 37, 61)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 16, 5)
+
+
+@pytest.mark.skipif(el.device_count() < 2, reason="needs >= 2 GPUs (one RCCL rank per GPU)")
+@pytest.mark.parametrize("world,height", [(2, 1), (2, 2)])
+def test_gpu_rccl_multi_gpu(world, height):
+    world = min(world, el.device_count())
+    _rccl_spawn(W.redist_worker, world, min(height, world), el.GPU, el.F64, 13, 11, 99)
+    algs = [el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT]
+    _rccl_spawn(W.gemm_worker, world, min(height, world), el.GPU, el.F64, [(45, 37, 61)], algs, 16, 6)
+
+
+def test_gpu_attach_torch_storage():
+    """ElementalMatrix::Attach on device memory owned by the caller (a torch
+    tensor): El::Gemm writes into it in place, padding rows untouched."""
+    import torch
+    m, n, k = 300, 200, 170
+    g = el.Grid()
+    Ah, Bh = oracle.hash_matrix(m, k, 1), oracle.hash_matrix(k, n, 2)
+    # column-major (ld x cols) == row-major (cols x ld) tensor
+    At = torch.from_numpy(np.ascontiguousarray(Ah.T)).cuda()
+    Bt = torch.from_numpy(np.ascontiguousarray(Bh.T)).cuda()
+    Ct = torch.full((n, m + 4), 3.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU).attach(m, k, 0, 0, At.data_ptr(), m)
+    B = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU).attach(k, n, 0, 0, Bt.data_ptr(), k)
+    C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU).attach(m, n, 0, 0, Ct.data_ptr(), m + 4)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, B, 0.0, C)
+    el.device_synchronize()
+    got = Ct.cpu().numpy().T
+    want = oracle.gemm("N", "N", 1.0, Ah, Bh, 0.0, np.zeros((m, n), order="F"))
+    assert oracle.parity_ratio(got[:m], want, Ah, Bh, k, np.finfo(np.float64).eps) <= 10
+    assert (got[m:] == 3.0).all()

@@ -1,0 +1,128 @@
+"""The oracle against the committed golden fixtures and known answers (CPU).
+
+tests/golden/*.npz are produced by tools/make_golden.py from the reference's
+definitions in plain Python integer arithmetic, independently of oracle.c;
+these tests pin the oracle before anything else is compared with it.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NAME = {"MC": oracle.MC, "MR": oracle.MR, "VC": oracle.VC, "VR": oracle.VR, "STAR": oracle.STAR,
+        "CIRC": oracle.CIRC}
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"))  # allow_pickle defaults to False
+
+
+def test_layout_matches_golden_every_rank():
+    z = _load("layout")
+    G = z["G"]
+    checked = 0
+    for key in z.files:
+        if key == "G":
+            continue
+        grid, U, V, a, ra, root, vc = key.split("_")
+        r, c = map(int, grid[1:].split("x"))
+        ca, ra_ = int(a[1:]), int(ra)
+        got = oracle.local_block(G, NAME[U], NAME[V], r, c, int(vc[2:]), ca, ra_, int(root[4:]))
+        want = z[key]
+        assert got.shape == want.shape, key
+        assert np.array_equal(got, want), key
+        checked += 1
+    assert checked == 336
+
+
+def test_layout_round_trip_place_block():
+    # scattering every rank's local block back reassembles the matrix (tests/core/DistMatrix.cpp:40-78)
+    G = oracle.hash_matrix(29, 17, 5)
+    for (U, V) in [(oracle.MC, oracle.MR), (oracle.VR, oracle.STAR), (oracle.STAR, oracle.VC),
+                   (oracle.MR, oracle.MC)]:
+        R = np.full_like(G, np.nan)
+        for vc in range(8):
+            oracle.place_block(R, oracle.local_block(G, U, V, 2, 4, vc, 1, 1), U, V, 2, 4, vc, 1, 1)
+        assert np.array_equal(R, G)
+
+
+@pytest.mark.parametrize("n,shift,stride,want", [(10, 3, 4, 2), (10, 0, 4, 3), (3, 3, 4, 0), (0, 0, 1, 0),
+                                                 (65536, 7, 8, 8192), (13, 1, 2, 6)])
+def test_length_known_answers(n, shift, stride, want):
+    assert oracle.length(n, shift, stride) == want
+
+
+def test_shift_and_default_height():
+    assert [oracle.shift(r, 2, 4) for r in range(4)] == [2, 3, 0, 1]
+    L = oracle.lib()
+    # Grid::DefaultHeight: largest divisor <= sqrt(p) (src/core/Grid.cpp:28-40)
+    assert [L.orc_default_height(p) for p in (1, 2, 3, 4, 6, 8, 12, 16)] == [1, 1, 1, 2, 2, 2, 3, 4]
+
+
+def test_hash_matches_golden():
+    z = _load("hash")
+    L = oracle.lib()
+    for seed in (1, 2, 3, 42):
+        got = np.array([L.orc_hash_unit(seed, int(i), int(j)) for i, j in z["ij"]])
+        assert np.array_equal(got, z[f"seed{seed}"]), seed
+    G = oracle.hash_matrix(5, 4, 2, 0.0, 0.1)
+    assert G[3, 2] == 0.0 + 0.1 * (2.0 * L.orc_hash_unit(2, 3, 2) - 1.0)
+
+
+@pytest.mark.parametrize("tag", ["NN", "NT", "TN", "TT"])
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_gemm_exact_golden(tag, dt):
+    z = _load("gemm_exact")
+    al, be = z["alpha_beta"]
+    got = oracle.gemm(tag[0], tag[1], al, z[f"{tag}_A"].astype(dt), z[f"{tag}_B"].astype(dt), be,
+                      z[f"{tag}_C"].astype(dt))
+    assert np.array_equal(got, z[f"{tag}_out"].astype(dt))
+
+
+@pytest.mark.parametrize("tag", ["NN", "TN"])
+def test_gemm_half_exact_golden(tag):
+    z = _load("gemm_exact")
+    al, be = z["alpha_beta"]
+    got = oracle.gemm_half(tag[0], tag[1], al, z[f"{tag}_A"], z[f"{tag}_B"], be, z[f"{tag}_C"])
+    assert np.array_equal(got.astype(np.float64), z[f"{tag}_out"])
+
+
+def test_gemm_beta_zero_never_reads_c():
+    A = oracle.hash_matrix(9, 7, 1)
+    B = oracle.hash_matrix(7, 5, 2)
+    C = np.full((9, 5), np.nan, order="F")
+    got = oracle.gemm("N", "N", 1.0, A, B, 0.0, C)
+    assert np.isfinite(got).all()
+
+
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("N", "T"), ("T", "N"), ("T", "T")])
+def test_gemm_vs_numpy(ta, tb):
+    m, n, k = 33, 21, 47
+    A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 1)
+    B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 2)
+    C = oracle.hash_matrix(m, n, 3)
+    got = oracle.gemm(ta, tb, 0.5, A, B, -0.5, C)
+    want = 0.5 * ((A if ta == "N" else A.T) @ (B if tb == "N" else B.T)) - 0.5 * C
+    assert oracle.parity_ratio(got, want, A, B, k, np.finfo(np.float64).eps) < 1.0
+
+
+@pytest.mark.parametrize("r,c,nb", [(1, 1, 128), (1, 2, 16), (2, 2, 7), (2, 4, 16), (3, 2, 5)])
+def test_summa_simulation_matches_gemm(r, c, nb):
+    m, n, k = 45, 38, 61
+    A = oracle.hash_matrix(m, k, 1)
+    B = oracle.hash_matrix(k, n, 2)
+    C = oracle.hash_matrix(m, n, 3)
+    got = oracle.summa_nnc(r, c, nb, 0.5, A, B, -0.5, C)
+    want = oracle.gemm("N", "N", 0.5, A, B, -0.5, C)
+    assert oracle.parity_ratio(got, want, A, B, k, np.finfo(np.float64).eps) < 1.0
+
+
+def test_bf16_rounding_known_answers():
+    x = np.array([1.0, 1.00390625, 1.005859375, -2.0, 3.0e38, np.inf], dtype=np.float32)
+    b = oracle.f32_to_bf16_bits(x)
+    # 1+2^-8 is a tie -> even (1.0); 1+1.5*2^-8 rounds up to 1+2^-7
+    assert list(oracle.bf16_bits_to_f32(b)[:4]) == [1.0, 1.0, 1.0078125, -2.0]
+    assert np.isinf(oracle.bf16_bits_to_f32(b)[5])
