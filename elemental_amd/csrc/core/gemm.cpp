@@ -124,7 +124,10 @@ Int EffectivePanel(const Grid& g, Int K) {
 //   op(A) panel: NORMAL -> A(:,k) as [MC,*];   TRANSPOSE -> A(k,:) as [*,MC]
 //   op(B) panel: NORMAL -> B(k,:) as [*,MR];   TRANSPOSE -> B(:,k) as [MR,*]
 // ---------------------------------------------------------------------------
-void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+// beta is folded into the first panel's update (the reference scales C in a
+// separate pass first, Gemm.cpp:282; one fewer HBM round trip of C here).
+void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
+            DistMatrix& CPre) {
     auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
@@ -197,19 +200,23 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         if (gpu) ELX_CHECK_HIP(hipStreamWaitEvent(cs, s.ready, 0));
         const Int m = C.LocalHeight(), n = C.LocalWidth();
         const Int k = IsN(oA) ? a.LocalWidth() : a.LocalHeight();
+        const double b_p = p == 0 ? beta : 1.0;
         if (m > 0 && n > 0 && k > 0) {
             const bool prof = gpu && Prof().on;
             Profiler::Rec rec{};
             if (prof) rec = Prof().Begin(cs);
             exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(), b.LDim(),
-                       1.0, C.Buffer(), C.LDim(), cs);
+                       b_p, C.Buffer(), C.LDim(), cs);
             if (prof) Prof().End(rec, cs, 2.0 * m * n * k, Prof().gemm);
+        } else if (p == 0) {
+            Scale(beta, C);
         }
         if (gpu) {
             ELX_CHECK_HIP(hipEventRecord(s.done, cs));
             s.pending = true;
         }
     };
+    if (np == 0) Scale(beta, C);
     if (np > 0) issue(0);
     for (int p = 0; p < np; ++p) {
         if (p + 1 < np) issue(p + 1);
@@ -440,12 +447,13 @@ void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B
     const Int kb = IsN(oB) ? B.Height() : B.Width(), n = IsN(oB) ? B.Width() : B.Height();
     ELX_REQUIRE(m == C.Height() && n == C.Width() && k == kb, "Gemm: nonconformal ", m, "x", k, " * ", kb, "x", n,
                 " -> ", C.Height(), "x", C.Width());
-    Scale(beta, C);  // Gemm.cpp:282
     if (alg == ELX_GEMM_DEFAULT) alg = Heuristic(m, n, k);
+    const bool fused_beta = alg == ELX_GEMM_SUMMA_C || alg == ELX_GEMM_SUMMA_C_MS;
+    if (!fused_beta) Scale(beta, C);  // Gemm.cpp:282
     switch (alg) {
     case ELX_GEMM_SUMMA_A_MS: case ELX_GEMM_SUMMA_A: SummaA(oA, oB, alpha, A, B, C); break;
     case ELX_GEMM_SUMMA_B_MS: case ELX_GEMM_SUMMA_B: SummaB(oA, oB, alpha, A, B, C); break;
-    case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, C); break;
+    case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, beta, C); break;
     case ELX_GEMM_SUMMA_DOT: SummaDot(oA, oB, alpha, A, B, C, kDotBlock); break;
     case ELX_GEMM_CANNON:
         throw UnsupportedError("GEMM_CANNON: the reference runs Cannon on the CPU only (NN.hpp:30-31); "

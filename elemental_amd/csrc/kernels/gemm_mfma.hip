@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 
 namespace elx {
 namespace kern {
@@ -68,6 +69,10 @@ struct GemmParams {
     const T* B; i64 ldb;
     T* C; i64 ldc;
     int tiles_m, tiles_n;
+    // split-k (gridDim.y = number of k chunks > 1): chunk z covers k in
+    // [z*kchunk, min(k, (z+1)*kchunk)) and writes its raw partial product to
+    // C + z*zstride (ldc = m, alpha = 1, beta = 0); splitk_reduce finishes.
+    i64 kchunk, zstride;
 };
 
 constexpr int BK = 16, GROUP_M = 8;
@@ -213,6 +218,13 @@ __global__ __launch_bounds__(CFG::NTHR, CFG::WAVES_PER_EU) void gemm_tile_kernel
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    {  // this workgroup's k chunk (the whole k unless split)
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += RA ? kz0 * p.lda : kz0;
+        p.B += RB ? kz0 * p.ldb : kz0;
+        p.C += (i64)blockIdx.y * p.zstride;
+    }
 
     acc_t acc[WM][WN];
 #pragma unroll
@@ -320,11 +332,75 @@ static hipError_t launch_cfg(GemmParams<T> p, hipStream_t s) {
     p.tiles_m = (int)((p.m + CFG::BM - 1) / CFG::BM);
     p.tiles_n = (int)((p.n + CFG::BN - 1) / CFG::BN);
     const int nwg = p.tiles_m * p.tiles_n;
+    const int nz = (int)((p.k + p.kchunk - 1) / p.kchunk);
     if (p.beta == T(0))
-        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, true, VEC, OFF32>), dim3(nwg), dim3(CFG::NTHR), 0, s, p);
+        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, true, VEC, OFF32>), dim3(nwg, nz), dim3(CFG::NTHR), 0, s, p);
     else
-        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, false, VEC, OFF32>), dim3(nwg), dim3(CFG::NTHR), 0, s, p);
+        hipLaunchKernelGGL((gemm_tile_kernel<T, CFG, TA, TB, false, VEC, OFF32>), dim3(nwg, nz), dim3(CFG::NTHR), 0, s, p);
     return hipGetLastError();
+}
+
+// C = alpha * sum_z W[z] + beta * C, z in order (deterministic); W[z] is m x n with ld m.
+template <typename T, bool BETA0>
+__global__ __launch_bounds__(256) void splitk_reduce(i64 m, i64 n, int nz, T alpha, const T* __restrict__ W, T beta,
+                                                     T* C, i64 ldc) {
+    const i64 mn = m * n;
+    for (i64 e = (i64)blockIdx.x * 256 + threadIdx.x; e < mn; e += (i64)gridDim.x * 256) {
+        T acc = W[e];
+        for (int z = 1; z < nz; ++z) acc += W[e + z * mn];
+        const i64 i = e % m, j = e / m;
+        T& o = C[i + j * ldc];
+        o = BETA0 ? alpha * acc : alpha * acc + beta * o;
+    }
+}
+
+// Split k when the output tiles alone cannot fill the chip (the Dot variant's
+// 2000 x 2000 x 524288 blocks, SUMMA_*Dot): aim for two rounds of resident
+// workgroups with chunks of >= 2048.  Returns the chunk count (1 = no split).
+template <typename CFG>
+static int split_count(i64 m, i64 n, i64 k) {
+    const i64 nwg = ((m + CFG::BM - 1) / CFG::BM) * ((n + CFG::BN - 1) / CFG::BN);
+    const i64 slots = 256 * CFG::MINB;  // resident workgroups on 256 CUs
+    if (nwg >= slots || k < 2 * 2048) return 1;
+    i64 z = (2 * slots + nwg - 1) / nwg;
+    z = std::min<i64>(z, k / 2048);
+    z = std::min<i64>(z, 16);
+    return (int)std::max<i64>(z, 1);
+}
+
+template <typename T, typename CFG, bool TA, bool TB, bool VEC, bool OFF32>
+static hipError_t launch_split(GemmParams<T> p, hipStream_t s) {
+    const int z = split_count<CFG>(p.m, p.n, p.k);
+    p.kchunk = std::max<i64>(p.k, 1);
+    p.zstride = 0;
+    if (z <= 1) return launch_cfg<T, CFG, TA, TB, VEC, OFF32>(p, s);
+    const i64 kchunk = ((p.k + z - 1) / z + BK - 1) / BK * BK;
+    const int nz = (int)((p.k + kchunk - 1) / kchunk);
+    T* W = nullptr;
+    const size_t bytes = sizeof(T) * (size_t)p.m * (size_t)p.n * (size_t)nz;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&W), bytes, s);
+    if (e != hipSuccess) return e;
+    GemmParams<T> q = p;
+    q.alpha = T(1);
+    q.beta = T(0);
+    q.C = W;
+    q.ldc = p.m;
+    q.kchunk = kchunk;
+    q.zstride = p.m * p.n;
+    e = launch_cfg<T, CFG, TA, TB, VEC, OFF32>(q, s);
+    if (e == hipSuccess) {
+        const i64 mn = p.m * p.n;
+        const int grid = (int)std::min<i64>((mn + 255) / 256, 256 * 16);
+        if (p.beta == T(0))
+            hipLaunchKernelGGL((splitk_reduce<T, true>), dim3(grid), dim3(256), 0, s, p.m, p.n, nz, p.alpha, W, p.beta,
+                               p.C, p.ldc);
+        else
+            hipLaunchKernelGGL((splitk_reduce<T, false>), dim3(grid), dim3(256), 0, s, p.m, p.n, nz, p.alpha, W, p.beta,
+                               p.C, p.ldc);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(W, s);
+    return e != hipSuccess ? e : f;
 }
 
 // Tile configuration (measured on MI355X, tools/variants.sh, 16384^3 NN):
@@ -350,22 +426,22 @@ static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
     const int tc = tile_choice<T>();
     if (off32) {
         switch (tc) {
-        case 256: return launch_cfg<T, Tile256, TA, TB, true, true>(p, s);
-        case 1288: return launch_cfg<T, Tile128w8, TA, TB, true, true>(p, s);
-        case 1289: return launch_cfg<T, Tile128w8n, TA, TB, true, true>(p, s);
-        case 12816: return launch_cfg<T, Tile128w16, TA, TB, true, true>(p, s);
-        case 2568: return launch_cfg<T, Tile256w8, TA, TB, true, true>(p, s);
-        default: return launch_cfg<T, Tile128, TA, TB, true, true>(p, s);
+        case 256: return launch_split<T, Tile256, TA, TB, true, true>(p, s);
+        case 1288: return launch_split<T, Tile128w8, TA, TB, true, true>(p, s);
+        case 1289: return launch_split<T, Tile128w8n, TA, TB, true, true>(p, s);
+        case 12816: return launch_split<T, Tile128w16, TA, TB, true, true>(p, s);
+        case 2568: return launch_split<T, Tile256w8, TA, TB, true, true>(p, s);
+        default: return launch_split<T, Tile128, TA, TB, true, true>(p, s);
         }
     }
-    if (vec) return launch_cfg<T, Tile128, TA, TB, true, false>(p, s);
-    return launch_cfg<T, Tile128, TA, TB, false, false>(p, s);
+    if (vec) return launch_split<T, Tile128, TA, TB, true, false>(p, s);
+    return launch_split<T, Tile128, TA, TB, false, false>(p, s);
 }
 
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s) {
-    GemmParams<T> p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0};
+    GemmParams<T> p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0, std::max<i64>(k, 1), 0};
     if (ta) return tb ? launch_tn<T, true, true>(p, s) : launch_tn<T, true, false>(p, s);
     return tb ? launch_tn<T, false, true>(p, s) : launch_tn<T, false, false>(p, s);
 }

@@ -36,7 +36,9 @@ def sync():
 
 
 OPS = {"N": L.NORMAL, "T": L.TRANSPOSE}
-SHAPES = [(1, 1, 1), (67, 53, 41), (128, 128, 16), (255, 257, 130), (300, 200, 517), (16, 700, 3)]
+SHAPES = [(1, 1, 1), (67, 53, 41), (128, 128, 16), (255, 257, 130), (300, 200, 517), (16, 700, 3),
+          # few output tiles, long k: split-k chunks + ordered reduce (even and odd k)
+          (96, 80, 9000), (67, 53, 4099)]
 
 
 @pytest.mark.parametrize("dt", ["f64", "f32"])
@@ -65,11 +67,13 @@ def test_local_gemm_f64_f32(dt, ta, tb):
             assert r <= 10, f"{dt} {ta}{tb} {m}x{n}x{k} beta={beta}: ratio {r}"
 
 
-def test_local_gemm_known_answer_exact():
+@pytest.mark.parametrize("k", [300, 8192])
+def test_local_gemm_known_answer_exact(k):
     """Integer-valued operands: every partial sum is exact in fp64, so the
-    product must match bit for bit whatever the summation order."""
+    product must match bit for bit whatever the summation order (k = 8192
+    takes the split-k path)."""
     rng = np.random.default_rng(0)
-    m, n, k = 130, 70, 300
+    m, n = 130, 70
     A = np.asfortranarray(rng.integers(-8, 8, (m, k)).astype(np.float64))
     B = np.asfortranarray(rng.integers(-8, 8, (k, n)).astype(np.float64))
     C = np.asfortranarray(rng.integers(-8, 8, (m, n)).astype(np.float64))
