@@ -1,0 +1,290 @@
+// 16-bit local GEMM, large-tile path for gfx950: C := alpha op(A) op(B) + beta C
+// (column-major, f32 accumulation, bf16 or f16 storage).
+//
+// Replaces rocblas_hgemm on the hot path (src/hydrogen/device/rocBLAS_API.cpp:151-170
+// via include/hydrogen/blas/GPU_BLAS_impl.hpp:397-423, LocalGemm at
+// src/blas_like/level3/Gemm.cpp:163-186) for the shapes SUMMA produces (config
+// C5: local 16384 x 8192 x kc panels).  Edges it does not take (k tail, small or
+// oddly aligned operands) go to the simple kernel of gemm_half.hip.
+//
+// Design (MI355X-first; cdna_hip_programming.md §5 "Canonical CDNA GEMM"):
+//  * 256 x 256 output tile per 512-thread workgroup (8 waves, 2 (M) x 4 (N)),
+//    each wave 128 x 64 = 8 x 4 accumulators of v_mfma_f32_16x16x32_{bf16,f16};
+//    BK = 64 per K-tile, one workgroup per CU.
+//  * Operands are staged HBM -> LDS with global_load_lds (16 B per lane, no
+//    VGPR round trip), two LDS stages of 64 KiB, the next K-tile in flight
+//    while the current one feeds the MFMAs.
+//  * Every orientation reads through the same two LDS image kinds:
+//      KC (k contiguous in HBM: op(A) = A^T, op(B) = B): rows of 64 k = 128 B,
+//         read with ds_read_b128 straight into the MFMA fragment;
+//      RC (rows contiguous: op(A) = A, op(B) = B^T): k-rows of 128 elements
+//         = 256 B, read with the gfx950 transposing ds_read_b64_tr_b16 (two
+//         per fragment), so no transpose pass and no extra HBM traffic.
+//    Both images are XOR-swizzled on the 16-B chunk index so the fragment
+//    reads are bank-conflict-free; the swizzle is applied to the GLOBAL source
+//    address of each glds lane (the LDS side of glds is lane-linear).
+//  * XCD-aware bijective workgroup remap (as gemm_mfma.hip).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.hpp"
+#include "elem.hpp"
+
+namespace elx {
+namespace kern {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) char lds_char;
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512, GROUP_M = 8;
+constexpr int HALF = 128 * BK * 2;  // one half-tile image: 128 rows x 64 k x 2 B = 16 KiB
+constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 0,1
+
+struct H2Params {
+    i64 m, n, k;  // k: multiple of BK
+    float alpha, beta;
+    const uint16_t* A; i64 lda;
+    const uint16_t* B; i64 ldb;
+    uint16_t* C; i64 ldc;
+    int tiles_m, tiles_n;
+    int vec_c;  // C base 8-B aligned and ldc % 4 == 0
+};
+
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int per_group = GROUP_M * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int inner = wg - group * per_group;
+    tm = first_m + inner % gsz;
+    tn = inner / gsz;
+}
+
+// XOR swizzles (16-B chunk index).  KC: 8 chunks per 128-B row, row r -> c ^ ((r>>1)&7):
+// the 16 lanes of a ds_read_b128 group (rows r..r+15 of one or two k-chunks) land
+// on 16 distinct 16-B bank slots.  RC: 16 chunks per 256-B k-row, k-row kk ->
+// c ^ (2(kk&3) + 8((kk>>3)&1)): the 8 k-rows x 32 B a 32-lane half of a
+// ds_read_b64_tr_b16 touches land on distinct bank slots; XOR values are even,
+// so the two chunks of a 32-B column pair stay adjacent.
+__device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int swz_rc(int kk) { return ((kk & 3) << 1) | (((kk >> 3) & 1) << 3); }
+
+__device__ __forceinline__ void glds16(const uint16_t* src, lds_char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// Stage one half-tile (128 operand rows starting at global row R, 64 k from k0)
+// into its LDS image.  16 wave-instructions of 1 KiB; wave w issues w and w+8.
+template <bool KC>
+__device__ __forceinline__ void stage_half(const uint16_t* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
+                                           int l) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ins = w + 8 * q;
+        if (KC) {  // X(row, k) = X[k + row*ld]; instruction = 8 rows of 128 B
+            const int r = ins * 8 + (l >> 3);
+            const int c = (l & 7) ^ swz_kc(r);
+            i64 row = R + r;
+            row = row < rows ? row : rows - 1;  // rows past the edge: any valid data (never stored)
+            glds16(X + row * ld + k0 + 8 * c, img + ins * 1024);
+        } else {   // X(row, k) = X[row + k*ld]; instruction = 4 k-rows of 256 B
+            const int kk = ins * 4 + (l >> 4);
+            const int c = (l & 15) ^ swz_rc(kk);
+            i64 col = R + 8 * c;
+            col = col <= rows - 8 ? col : rows - 8;
+            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+        }
+    }
+}
+
+// One MFMA operand fragment (16 operand rows from R0, k-step s of 32):
+// lane l holds X(R0 + (l&15), 32s + 8(l>>4) + j), j = 0..7.
+template <bool KC>
+__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l) {
+    if (KC) {
+        const int row = R0 + (l & 15), c = 4 * s + (l >> 4);
+        return *(const __attribute__((address_space(3))) u32x4*)(img + row * 128 + ((c ^ swz_kc(row)) << 4));
+    } else {
+        const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+        const int c = (R0 >> 3) + (p >> 1);
+        u32x4 out;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = 32 * s + 8 * g + 4 * h + q;
+            const lds_char* a = img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3);
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+            const u32x2 u = __builtin_bit_cast(u32x2, v);
+            out[2 * h] = u[0];
+            out[2 * h + 1] = u[1];
+        }
+        return out;
+    }
+}
+
+template <bool BF16>
+__device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
+    if constexpr (BF16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                       0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                      0, 0);
+}
+
+struct Frame {  // per-workgroup constants of the main loop
+    const uint16_t* A; i64 lda, m, m0;
+    const uint16_t* B; i64 ldb, n, n0;
+    int w, l, wr, wc;
+};
+
+// One main-loop step: stage K-tile t+1 into `next` (if any) and run the MFMAs of
+// the K-tile already in `cur`.  The two LDS pointers are __restrict__ so the
+// inlined accesses carry alias scopes: hipcc's waitcnt pass then knows the
+// in-flight glds writes cannot alias the ds_reads and does not wait vmcnt(0)
+// before them (without the scopes every ds_read would drain the prefetch).
+template <bool BF16, bool KCA, bool KCB>
+__device__ __forceinline__ void step(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
+                                     const lds_char* __restrict__ cur, f32x4 (&acc)[8][4]) {
+    if (more) {
+        stage_half<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_half<KCA>(f.A, f.lda, f.m, f.m0 + 128, knext, next + HALF, f.w, f.l);
+        stage_half<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + 2 * HALF, f.w, f.l);
+        stage_half<KCB>(f.B, f.ldb, f.n, f.n0 + 128, knext, next + 3 * HALF, f.w, f.l);
+    }
+    const lds_char* Ah = cur + f.wr * HALF;
+    const lds_char* Bh = cur + 2 * HALF + (f.wc >> 1) * HALF;
+    const int bc = (f.wc & 1) * 64;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+        u32x4 a[8], b[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b[ni] = frag<KCB>(Bh, bc + ni * 16, s, f.l);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = frag<KCA>(Ah, mi * 16, s, f.l);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma<BF16>(a[mi], b[ni], acc[mi][ni]);
+    }
+}
+
+// KCA: op(A) k-contiguous (TA); KCB: op(B) k-contiguous (!TB).
+template <bool BF16, bool KCA, bool KCB>
+__global__ __launch_bounds__(NT, 1) void gemm_h256_kernel(H2Params p) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;  // generic -> LDS address space
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    stage_half<KCA>(f.A, f.lda, f.m, m0, 0, lds, w, l);
+    stage_half<KCA>(f.A, f.lda, f.m, m0 + 128, 0, lds + HALF, w, l);
+    stage_half<KCB>(f.B, f.ldb, f.n, n0, 0, lds + 2 * HALF, w, l);
+    stage_half<KCB>(f.B, f.ldb, f.n, n0 + 128, 0, lds + 3 * HALF, w, l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        step<BF16, KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        // the staged K-tile has landed and every wave is done reading the other
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // Epilogue: C/D map of 16x16x32: col = lane&15, rows 4*(lane>>4) + r (r = 0..3),
+    // i.e. four consecutive rows of one column = one 8-B access per tile.
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 64 + (l & 15);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const i64 i = rb + mi * 16, j = cb + ni * 16;
+            if (j >= p.n || i >= p.m) continue;
+            uint16_t* o = p.C + i + j * p.ldc;
+            if (p.vec_c && i + 3 < p.m) {
+                uint2 cv = make_uint2(0, 0);
+                if (p.beta != 0.f) cv = *reinterpret_cast<const uint2*>(o);
+                const uint16_t in[4] = {(uint16_t)(cv.x & 0xffff), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xffff),
+                                        (uint16_t)(cv.y >> 16)};
+                uint16_t r16[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = p.alpha * acc[mi][ni][r];
+                    if (p.beta != 0.f) v += p.beta * E::load(in[r]);
+                    r16[r] = E::store(v);
+                }
+                *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16),
+                                                          (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (i + r >= p.m) break;
+                    float v = p.alpha * acc[mi][ni][r];
+                    if (p.beta != 0.f) v += p.beta * E::load(o[r]);
+                    o[r] = E::store(v);
+                }
+            }
+        }
+    }
+}
+
+template <bool BF16, bool KCA, bool KCB>
+hipError_t launch_h256(const H2Params& p, hipStream_t s) {
+    hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
+    return hipGetLastError();
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+}  // namespace
+
+hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
+                       i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
+    const bool kca = ta, kcb = !tb;
+    const i64 kmain = k / BK * BK;
+    // the large-tile path: 16-B aligned rows/columns for glds, RC operands a
+    // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
+    const bool ok = kmain > 0 && al16(A) && al16(B) && lda % 8 == 0 && ldb % 8 == 0 &&
+                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) &&
+                    ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 64 && m < (1ll << 31) && n < (1ll << 31);
+    if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
+    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0};
+    hipError_t e;
+    if (is_bf16) {
+        if (kca) e = kcb ? launch_h256<true, true, true>(p, s) : launch_h256<true, true, false>(p, s);
+        else e = kcb ? launch_h256<true, false, true>(p, s) : launch_h256<true, false, false>(p, s);
+    } else {
+        if (kca) e = kcb ? launch_h256<false, true, true>(p, s) : launch_h256<false, true, false>(p, s);
+        else e = kcb ? launch_h256<false, false, true>(p, s) : launch_h256<false, false, false>(p, s);
+    }
+    if (e != hipSuccess || kmain == k) return e;
+    // k tail (< 64): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
+    const uint16_t* At = ta ? A + kmain : A + kmain * lda;
+    const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
+    return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);
+}
+
+}  // namespace kern
+}  // namespace elx

@@ -168,7 +168,7 @@ hipError_t launch(const HParams& p, hipStream_t s) {
 
 }  // namespace
 
-hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
+hipError_t gemm_mfma_h_simple(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
     HParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN)};
     if (is_bf16) {

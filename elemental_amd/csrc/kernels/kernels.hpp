@@ -15,6 +15,10 @@ hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A,
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
                        const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
                        uint16_t* C, i64 ldc, hipStream_t s);
+// the 128x128-tile kernel every shape can take (edges, k tails, small problems)
+hipError_t gemm_mfma_h_simple(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
+                              const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
+                              uint16_t* C, i64 ldc, hipStream_t s);
 
 // One strided 2-D block move: dst(i,j) (=|+=) alpha*src(i,j),
 // src(i,j) = src[i*scs + j*srs], dst(i,j) = dst[i*dcs + j*drs].

@@ -87,8 +87,11 @@ def test_local_gemm_known_answer_exact(k):
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-def test_local_gemm_16bit(kind, ta, tb):
-    m, n, k = 131, 77, 95
+@pytest.mark.parametrize("shape", [(131, 77, 95), (2000, 2056, 200)])
+def test_local_gemm_16bit(kind, ta, tb, shape):
+    """(131, 77, 95): the 128x128 kernel; (2000, 2056, 200): the 256x256
+    glds/transposed-read kernel with ragged edge tiles plus the k-tail pass."""
+    m, n, k = shape
     if kind == "f16":
         A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 21, 0, 1, np.float16)
         B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 22, 0, 1, np.float16)
@@ -111,7 +114,7 @@ def test_local_gemm_16bit(kind, ta, tb):
     gotf = got.astype(np.float64) if kind == "f16" else oracle.bf16_bits_to_f32(got).astype(np.float64)
     r = oracle.parity_ratio(gotf, exact, Af, Bf, k, eps)
     assert r <= 10, f"{kind} {ta}{tb}: ratio {r}"
-    if kind == "f16":
+    if kind == "f16" and m * n * k < 2e6:  # (the half-path oracle is a Python loop nest)
         # never worse than the reference's own CPU half path (half accumulation)
         refh = oracle.gemm_half(ta, tb, 0.5, A, B, -0.5, C).astype(np.float64)
         assert np.linalg.norm(gotf - exact) <= np.linalg.norm(refh - exact) + 1e-3
