@@ -19,6 +19,9 @@
 #include "kernels.hpp"
 #include "elem.hpp"
 #include "../../../include/elemental_amd.h"
+#include <algorithm>
+#include <initializer_list>
+#include <utility>
 
 namespace elx {
 namespace kern {
@@ -27,6 +30,7 @@ namespace {
 
 constexpr int TILE = 64;
 constexpr int NT = 256;
+constexpr int UNROLL = 4;  // vectors in flight per lane in the elementwise engine
 
 struct CopyBatch {
     Copy2D d[kMaxCopyBatch];
@@ -87,36 +91,183 @@ __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
     }
 }
 
-// 2-D elementwise driver: columns over gridDim.y, rows over gridDim.x*NT.
+// Vectorized 2-D elementwise engine (HBM-bound ops).  Columns over gridDim.y,
+// rows over gridDim.x*NT lanes, each lane moving VEC = 16 B / sizeof(S)
+// elements per access (one global_load/store_dwordx4) when every operand's
+// column starts are 16-B aligned (uniform per launch); otherwise element by
+// element.  The host collapses contiguous operands (ld == m) into one column.
+template <typename S>
+struct V16 {
+    static constexpr int N = 16 / sizeof(S);
+    S v[N];
+};
+
+// Operand 0 is the output; RD0 says whether the op reads it (scale) or only
+// writes it (fill, hadamard, map), so no HBM read is spent on a pure output.
+template <typename S, int NOP, bool RD0, typename F>
+__device__ __forceinline__ void ew_2d(i64 m, i64 n, S* const (&ptr)[NOP], const i64 (&ld)[NOP], bool vec, F&& f) {
+    constexpr int N = V16<S>::N;
+    constexpr i64 CHUNK = (i64)NT * UNROLL * N;  // elements per workgroup pass of a column
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
+        S* col[NOP];
+#pragma unroll
+        for (int q = 0; q < NOP; ++q) col[q] = ptr[q] + j * ld[q];
+        for (i64 c0 = (i64)blockIdx.x * CHUNK; c0 < m; c0 += (i64)gridDim.x * CHUNK) {
+            if (vec && c0 + CHUNK <= m) {
+                // UNROLL independent 16-B accesses per operand in flight per lane,
+                // the workgroup sweeping one contiguous CHUNK
+                V16<S> x[NOP][UNROLL];
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                    for (int q = RD0 ? 0 : 1; q < NOP; ++q)
+                        x[q][u] = *reinterpret_cast<const V16<S>*>(col[q] + c0 + (u * NT + threadIdx.x) * N);
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                    for (int e = 0; e < N; ++e) {
+                        S r[NOP];
+#pragma unroll
+                        for (int q = RD0 ? 0 : 1; q < NOP; ++q) r[q] = x[q][u].v[e];
+                        x[0][u].v[e] = f(r);
+                    }
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u)
+                    *reinterpret_cast<V16<S>*>(col[0] + c0 + (u * NT + threadIdx.x) * N) = x[0][u];
+            } else {
+                const i64 end = c0 + CHUNK < m ? c0 + CHUNK : m;
+                for (i64 i = c0 + (i64)threadIdx.x * N; i < end; i += (i64)NT * N) {
+                    if (vec && i + N <= end) {
+                        V16<S> x[NOP];
+#pragma unroll
+                        for (int q = RD0 ? 0 : 1; q < NOP; ++q) x[q] = *reinterpret_cast<const V16<S>*>(col[q] + i);
+#pragma unroll
+                        for (int e = 0; e < N; ++e) {
+                            S r[NOP];
+#pragma unroll
+                            for (int q = RD0 ? 0 : 1; q < NOP; ++q) r[q] = x[q].v[e];
+                            x[0].v[e] = f(r);
+                        }
+                        *reinterpret_cast<V16<S>*>(col[0] + i) = x[0];
+                    } else {
+                        for (i64 e = i; e < i + N && e < end; ++e) {
+                            S r[NOP];
+#pragma unroll
+                            for (int q = RD0 ? 0 : 1; q < NOP; ++q) r[q] = col[q][e];
+                            col[0][e] = f(r);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Batched column-contiguous moves (scs == dcs == 1: axpy, copy, and every
+// pack/unpack whose portions are whole column runs): the descriptor's
+// n x ceil(m/VEC) vectors are dealt over the workgroups of its blockIdx.y row.
+template <typename T, bool AXPY>
+__global__ __launch_bounds__(NT) void copy_cols_kernel(CopyBatch b, double alpha) {
+    using E = Elem<T>;
+    using S = typename E::storage;
+    constexpr int N = V16<S>::N;
+    const Copy2D& d = b.d[blockIdx.y];
+    const S* src = static_cast<const S*>(d.src);
+    S* dst = static_cast<S*>(d.dst);
+    const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16 == 0) &&
+                     ((d.srs * (i64)sizeof(S)) % 16 == 0 || d.n == 1) && ((d.drs * (i64)sizeof(S)) % 16 == 0 || d.n == 1);
+    const auto a = (typename E::compute)alpha;
+    const i64 mv = (d.m + N - 1) / N, total = mv * d.n;
+    auto one = [&](i64 id) {
+        const i64 j = id / mv, i = (id - j * mv) * N;
+        const S* x = src + j * d.srs + i;
+        S* y = dst + j * d.drs + i;
+        if (vec && i + N <= d.m) {
+            const V16<S> xv = *reinterpret_cast<const V16<S>*>(x);
+            if (AXPY) {
+                V16<S> yv = *reinterpret_cast<const V16<S>*>(y);
+#pragma unroll
+                for (int e = 0; e < N; ++e) yv.v[e] = E::store(E::load(yv.v[e]) + a * E::load(xv.v[e]));
+                *reinterpret_cast<V16<S>*>(y) = yv;
+            } else {
+                *reinterpret_cast<V16<S>*>(y) = xv;
+            }
+        } else {
+            for (i64 e = 0; e < N && i + e < d.m; ++e) {
+                if (AXPY) y[e] = E::store(E::load(y[e]) + a * E::load(x[e]));
+                else y[e] = x[e];
+            }
+        }
+    };
+    constexpr i64 CHUNK = (i64)NT * UNROLL;  // vectors per workgroup pass
+    for (i64 c0 = (i64)blockIdx.x * CHUNK; c0 < total; c0 += (i64)gridDim.x * CHUNK) {
+        if (vec && d.m % N == 0 && c0 + CHUNK <= total) {
+            // every vector whole: UNROLL independent loads in flight before any store
+            V16<S> xv[UNROLL], yv[UNROLL];
+            S* y[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const i64 k = c0 + u * NT + threadIdx.x, j = k / mv, i = (k - j * mv) * N;
+                xv[u] = *reinterpret_cast<const V16<S>*>(src + j * d.srs + i);
+                y[u] = dst + j * d.drs + i;
+                if (AXPY) yv[u] = *reinterpret_cast<const V16<S>*>(y[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                if (AXPY) {
+#pragma unroll
+                    for (int e = 0; e < N; ++e) yv[u].v[e] = E::store(E::load(yv[u].v[e]) + a * E::load(xv[u].v[e]));
+                    *reinterpret_cast<V16<S>*>(y[u]) = yv[u];
+                } else {
+                    *reinterpret_cast<V16<S>*>(y[u]) = xv[u];
+                }
+            }
+        } else {
+            for (i64 k = c0 + threadIdx.x; k < c0 + CHUNK && k < total; k += NT) one(k);
+        }
+    }
+}
+
+// 2-D elementwise driver (fill_hash): columns over gridDim.y, rows over gridDim.x*NT.
 template <typename F>
 __device__ __forceinline__ void for_each_2d(i64 m, i64 n, F&& f) {
     for (i64 j = blockIdx.y; j < n; j += gridDim.y)
         for (i64 i = (i64)blockIdx.x * NT + threadIdx.x; i < m; i += (i64)gridDim.x * NT) f(i, j);
 }
 
+// operand 0 is the output (read too by scale; for fill/hadamard/map its value is ignored)
 template <typename T>
-__global__ __launch_bounds__(NT) void fill_kernel(i64 m, i64 n, double v, typename Elem<T>::storage* A, i64 lda) {
+__global__ __launch_bounds__(NT) void fill_kernel(i64 m, i64 n, double v, typename Elem<T>::storage* A, i64 lda,
+                                                  bool vec) {
     using E = Elem<T>;
-    const auto s = E::store((typename E::compute)v);
-    for_each_2d(m, n, [&](i64 i, i64 j) { A[i + j * lda] = s; });
+    using S = typename E::storage;
+    const S s = E::store((typename E::compute)v);
+    S* const p[1] = {A};
+    const i64 l[1] = {lda};
+    ew_2d<S, 1, false>(m, n, p, l, vec, [&](const S(&)[1]) { return s; });
 }
 
 template <typename T>
-__global__ __launch_bounds__(NT) void scale_kernel(i64 m, i64 n, double alpha, typename Elem<T>::storage* A, i64 lda) {
+__global__ __launch_bounds__(NT) void scale_kernel(i64 m, i64 n, double alpha, typename Elem<T>::storage* A, i64 lda,
+                                                   bool vec) {
     using E = Elem<T>;
+    using S = typename E::storage;
     const auto a = (typename E::compute)alpha;
-    for_each_2d(m, n, [&](i64 i, i64 j) { auto& x = A[i + j * lda]; x = E::store(a * E::load(x)); });
+    S* const p[1] = {A};
+    const i64 l[1] = {lda};
+    ew_2d<S, 1, true>(m, n, p, l, vec, [&](const S(&x)[1]) { return E::store(a * E::load(x[0])); });
 }
 
 template <typename T>
 __global__ __launch_bounds__(NT) void hadamard_kernel(i64 m, i64 n, const typename Elem<T>::storage* A, i64 lda,
                                                       const typename Elem<T>::storage* B, i64 ldb,
-                                                      typename Elem<T>::storage* C, i64 ldc) {
+                                                      typename Elem<T>::storage* C, i64 ldc, bool vec) {
     using E = Elem<T>;
+    using S = typename E::storage;
     // in-place aliasing (C==A or C==B) is safe: each element is read before its own write
-    for_each_2d(m, n, [&](i64 i, i64 j) {
-        C[i + j * ldc] = E::store(E::load(A[i + j * lda]) * E::load(B[i + j * ldb]));
-    });
+    S* const p[3] = {C, const_cast<S*>(A), const_cast<S*>(B)};
+    const i64 l[3] = {ldc, lda, ldb};
+    ew_2d<S, 3, false>(m, n, p, l, vec, [&](const S(&x)[3]) { return E::store(E::load(x[1]) * E::load(x[2])); });
 }
 
 template <typename C>
@@ -139,9 +290,12 @@ __device__ __forceinline__ C apply_map(int fn, C x) {
 
 template <typename T, int FN>
 __global__ __launch_bounds__(NT) void map_kernel(i64 m, i64 n, const typename Elem<T>::storage* A, i64 lda,
-                                                 typename Elem<T>::storage* B, i64 ldb) {
+                                                 typename Elem<T>::storage* B, i64 ldb, bool vec) {
     using E = Elem<T>;
-    for_each_2d(m, n, [&](i64 i, i64 j) { B[i + j * ldb] = E::store(apply_map(FN, E::load(A[i + j * lda]))); });
+    using S = typename E::storage;
+    S* const p[2] = {B, const_cast<S*>(A)};
+    const i64 l[2] = {ldb, lda};
+    ew_2d<S, 2, false>(m, n, p, l, vec, [&](const S(&x)[2]) { return E::store(apply_map(FN, E::load(x[1]))); });
 }
 
 template <typename T>
@@ -158,6 +312,30 @@ __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>
         const double v = center + radius * (2.0 * u - 1.0);
         A[i + j * lda] = E::store((typename E::compute)v);  // double -> compute (RNE) -> storage (RNE)
     });
+}
+
+// Launch geometry of ew_2d: collapse to one column when every operand is
+// contiguous (ld == m), and decide the 16-B vector path.
+struct EwShape {
+    i64 m, n;
+    bool vec;
+    dim3 grid;
+};
+template <typename S>
+EwShape ew_shape(i64 m, i64 n, std::initializer_list<std::pair<const void*, i64>> ops) {
+    bool contig = true, vec = true;
+    for (auto& o : ops) {
+        contig = contig && (o.second == m || n == 1);
+        vec = vec && (reinterpret_cast<uintptr_t>(o.first) % 16 == 0);
+    }
+    if (contig) { m *= n; n = 1; }
+    for (auto& o : ops) vec = vec && (n == 1 || (o.second * (i64)sizeof(S)) % 16 == 0);
+    constexpr int N = 16 / sizeof(S);
+    // one pass: every workgroup sweeps one CHUNK of one column
+    i64 gx = (m + (i64)NT * N * UNROLL - 1) / ((i64)NT * N * UNROLL);
+    const i64 gy = n < 1 ? 1 : (n > 65535 ? 65535 : n);
+    gx = std::max<i64>(1, std::min<i64>(gx, (1ll << 31) - 1));
+    return EwShape{m, n, vec, dim3((unsigned)gx, (unsigned)gy)};
 }
 
 dim3 grid2d(i64 m, i64 n) {
@@ -184,21 +362,35 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
     for (int base = 0; base < nd; base += kMaxCopyBatch) {
         CopyBatch b{};
         const int cnt = (nd - base) < kMaxCopyBatch ? (nd - base) : kMaxCopyBatch;
-        i64 maxtiles = 0;
+        i64 maxtiles = 0, maxvec = 0;
         int used = 0;
+        bool cols = true;
+        const int es = dtype == ELX_F64 ? 8 : dtype == ELX_F32 ? 4 : 2;
         for (int q = 0; q < cnt; ++q) {
             const Copy2D& x = d[base + q];
             if (x.m <= 0 || x.n <= 0) continue;
             b.d[used++] = x;
             const i64 t = ((x.m + TILE - 1) / TILE) * ((x.n + TILE - 1) / TILE);
             if (t > maxtiles) maxtiles = t;
+            const i64 v = (x.m + 16 / es - 1) / (16 / es) * x.n;
+            if (v > maxvec) maxvec = v;
+            cols = cols && x.scs == 1 && x.dcs == 1;
         }
         if (used == 0) continue;
-        const unsigned gx = (unsigned)(maxtiles > 4096 ? 4096 : maxtiles);
-        dim3 grid(gx, used);
-        ELX_DTYPE_SWITCH(dtype, T,
-            if (axpy) hipLaunchKernelGGL((copy2d_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
-            else hipLaunchKernelGGL((copy2d_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
+        if (cols) {
+            // ~16 workgroups per CU across the batch
+            const i64 gx = std::max<i64>(1, std::min<i64>((maxvec + NT * UNROLL - 1) / (NT * UNROLL), 1 << 20));
+            dim3 grid((unsigned)gx, used);
+            ELX_DTYPE_SWITCH(dtype, T,
+                if (axpy) hipLaunchKernelGGL((copy_cols_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
+                else hipLaunchKernelGGL((copy_cols_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
+        } else {
+            const unsigned gx = (unsigned)(maxtiles > 4096 ? 4096 : maxtiles);
+            dim3 grid(gx, used);
+            ELX_DTYPE_SWITCH(dtype, T,
+                if (axpy) hipLaunchKernelGGL((copy2d_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
+                else hipLaunchKernelGGL((copy2d_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -207,17 +399,21 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
 
 hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return hipSuccess;
-    ELX_DTYPE_SWITCH(dtype, T,
-        hipLaunchKernelGGL((fill_kernel<T>), grid2d(m, n), dim3(NT), 0, s, m, n, v,
-                           static_cast<typename Elem<T>::storage*>(A), lda));
+    ELX_DTYPE_SWITCH(dtype, T, {
+        const EwShape g = ew_shape<typename Elem<T>::storage>(m, n, {{A, lda}});
+        hipLaunchKernelGGL((fill_kernel<T>), g.grid, dim3(NT), 0, s, g.m, g.n, v,
+                           static_cast<typename Elem<T>::storage*>(A), lda, g.vec);
+    });
     return hipGetLastError();
 }
 
 hipError_t scale2d(int dtype, i64 m, i64 n, double alpha, void* A, i64 lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return hipSuccess;
-    ELX_DTYPE_SWITCH(dtype, T,
-        hipLaunchKernelGGL((scale_kernel<T>), grid2d(m, n), dim3(NT), 0, s, m, n, alpha,
-                           static_cast<typename Elem<T>::storage*>(A), lda));
+    ELX_DTYPE_SWITCH(dtype, T, {
+        const EwShape g = ew_shape<typename Elem<T>::storage>(m, n, {{A, lda}});
+        hipLaunchKernelGGL((scale_kernel<T>), g.grid, dim3(NT), 0, s, g.m, g.n, alpha,
+                           static_cast<typename Elem<T>::storage*>(A), lda, g.vec);
+    });
     return hipGetLastError();
 }
 
@@ -226,25 +422,26 @@ hipError_t hadamard2d(int dtype, i64 m, i64 n, const void* A, i64 lda, const voi
     if (m <= 0 || n <= 0) return hipSuccess;
     ELX_DTYPE_SWITCH(dtype, T, {
         using S = typename Elem<T>::storage;
-        hipLaunchKernelGGL((hadamard_kernel<T>), grid2d(m, n), dim3(NT), 0, s, m, n,
+        const EwShape g = ew_shape<S>(m, n, {{A, lda}, {B, ldb}, {C, ldc}});
+        hipLaunchKernelGGL((hadamard_kernel<T>), g.grid, dim3(NT), 0, s, g.m, g.n,
                            static_cast<const S*>(A), lda, static_cast<const S*>(B), ldb,
-                           static_cast<S*>(C), ldc);
+                           static_cast<S*>(C), ldc, g.vec);
     });
     return hipGetLastError();
 }
 
 template <typename T, int FN>
-static void launch_map(dim3 g, hipStream_t s, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb) {
+static void launch_map(hipStream_t s, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb) {
     using S = typename Elem<T>::storage;
-    hipLaunchKernelGGL((map_kernel<T, FN>), g, dim3(NT), 0, s, m, n, static_cast<const S*>(A), lda,
-                       static_cast<S*>(B), ldb);
+    const EwShape g = ew_shape<S>(m, n, {{A, lda}, {B, ldb}});
+    hipLaunchKernelGGL((map_kernel<T, FN>), g.grid, dim3(NT), 0, s, g.m, g.n, static_cast<const S*>(A), lda,
+                       static_cast<S*>(B), ldb, g.vec);
 }
 
 hipError_t entrywise_map(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb,
                          hipStream_t s) {
     if (m <= 0 || n <= 0) return hipSuccess;
-    const dim3 g = grid2d(m, n);
-#define ELX_MAP_CASE(F) case F: launch_map<T, F>(g, s, m, n, A, lda, B, ldb); break;
+#define ELX_MAP_CASE(F) case F: launch_map<T, F>(s, m, n, A, lda, B, ldb); break;
     ELX_DTYPE_SWITCH(dtype, T, switch (fn) {
         ELX_MAP_CASE(ELX_MAP_IDENTITY) ELX_MAP_CASE(ELX_MAP_NEGATE) ELX_MAP_CASE(ELX_MAP_ABS)
         ELX_MAP_CASE(ELX_MAP_SQUARE) ELX_MAP_CASE(ELX_MAP_SQRT) ELX_MAP_CASE(ELX_MAP_EXP)
