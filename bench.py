@@ -1,24 +1,30 @@
 #!/usr/bin/env python3
 """Headline benchmark: distributed El::Gemm TFLOP/s on MI355X (BASELINE.json metric).
 
-  python bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --steps K --warmup W [--config c2|c3|c4|c5]
   (N > 1: launched by torch.distributed.run, one process per GPU; RANK /
    LOCAL_RANK / WORLD_SIZE / MASTER_* come from the environment)
 
-One step = one El::Gemm(NORMAL, NORMAL, alpha=0.5, A, B, beta=-0.5, C) on
-DistMatrix<double,MC,MR,ELEMENT,GPU> operands already resident in HBM,
-inputs Uniform(-0.1, 0.1) as tests/blas_like/Gemm_Suite.cpp:158-172 (from the
-grid-independent counter hash, synthetic data).  The whole SUMMA runs inside
-the timed region: Scale(beta, C), every panel redistribution over RCCL, every
-MFMA update.
-  N = 1 : config C2, m=n=k=32768 on a 1x1 grid (BASELINE.json configs[1]).
-  N > 1 : config C3, m=n=k=65536 on Grid::DefaultHeight(N) (1x2, 2x2, 2x4):
-          strong scaling of the same problem.
+One step = one El::Gemm(...) on DistMatrix operands already resident in HBM,
+inputs from the grid-independent counter hash (synthetic data, Uniform(-0.1,
+0.1) as tests/blas_like/Gemm_Suite.cpp:158-172, alpha = 0.5, beta = -0.5).
+The whole SUMMA runs inside the timed region: every panel redistribution over
+RCCL and every MFMA update (beta is folded into the first panel's update).
+Default workload (the driver's line):
+  N = 1 : C2, El::Gemm NN fp64 m=n=k=32768 on a 1x1 grid (BASELINE.json configs[1]).
+  N > 1 : C3, SUMMA El::Gemm NN fp64 m=n=k=65536 on Grid::DefaultHeight(N)
+          (1x2, 2x2, 2x4): strong scaling of the same problem.
+Extra lines (evidence, not the driver's default):
+  --config c4 : TN fp32 m=n=8192, k=524288*N, inputs [VC,STAR] (LBANN's
+                weight-gradient shape, SUMMA_DOT); weak scaling, = C4 at N=8.
+  --config c5 : NN bf16 (or --dtype f16) m=n=k=32768 on [MC,MR], plus
+                DistMatrix Axpy and Hadamard on the same operands (GB/s).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -27,34 +33,34 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X dense MFMA, datasheet (MI355X_MICROARCH.md / SURVEY §6)
+# MI355X dense peaks (MI355X_MICROARCH.md: fp64/fp32 MFMA = vector rate; bf16/f16 2.5 PF dense)
+PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3, "bf16": 2500.0, "f16": 2500.0}
+HBM_PEAK_GBS = 8000.0
+METRIC = "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak"
+KERNEL = {"f64": "gemm_tile_kernel<double>", "f32": "gemm_tile_kernel<float>",
+          "bf16": "gemm_h256_kernel<bf16>", "f16": "gemm_h256_kernel<f16>"}
 
 
-def cpu_baseline(seconds_target: float = 15.0) -> dict:
-    """The oracle's CPU GEMM (oracle/oracle.c, the reference's loop nest), single
-    thread, on a bounded sample of the same workload: an NN fp64 GEMM of
-    s x s x s with the same input distribution, s grown until ~seconds_target."""
-    import numpy as np
+def cpu_baseline(seconds_target: float = 10.0) -> dict:
+    """The CPU leg (oracle/cpu_gemm.c: blocked, packed, OpenMP f64 GEMM standing
+    in for the reference's multi-threaded BLAS dgemm of its CPU path) on the
+    host's cores, on a bounded sample of the same workload: NN fp64 s x s x s
+    with the same input distribution, repeated for ~seconds_target."""
     import oracle
-    s, t = 256, 0.0
-    while True:
-        A = oracle.hash_matrix(s, s, 1, 0.0, 0.1)
-        B = oracle.hash_matrix(s, s, 2, 0.0, 0.1)
-        C = oracle.hash_matrix(s, s, 3, 0.0, 0.1)
+    s = 4096
+    A = oracle.hash_matrix(s, s, 1, 0.0, 0.1)
+    B = oracle.hash_matrix(s, s, 2, 0.0, 0.1)
+    C = oracle.hash_matrix(s, s, 3, 0.0, 0.1)
+    oracle.cpu_gemm("N", "N", 0.5, A, B, -0.5, C)  # warm-up (thread pool, pages)
+    reps, total = 0, 0.0
+    while total < seconds_target:
         t0 = time.perf_counter()
-        oracle.gemm("N", "N", 0.5, A, B, -0.5, C)
-        t = time.perf_counter() - t0
-        if t * 8 > seconds_target or s >= 4096:
-            break
-        s *= 2
-    reps, total = 1, t
-    while total < 10.0:  # about 10-30 s of CPU work in all
-        t0 = time.perf_counter()
-        oracle.gemm("N", "N", 0.5, A, B, -0.5, C)
+        oracle.cpu_gemm("N", "N", 0.5, A, B, -0.5, C)
         total += time.perf_counter() - t0
         reps += 1
-    return {"value": 2.0 * s ** 3 * reps / total / 1e12, "unit": "TFLOP/s", "cores": 1, "kind": "port",
-            "sample": f"oracle C GEMM NN fp64 {s}x{s}x{s} x{reps}, 1 thread, {total:.2f} s"}
+    cores = oracle.cpu_threads()
+    return {"value": round(2.0 * s ** 3 * reps / total / 1e12, 4), "unit": "TFLOP/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/cpu_gemm.c blocked OpenMP dgemm NN fp64 {s}^3 x{reps}, {cores} threads, {total:.1f} s"}
 
 
 def measured_traffic(dtype: str, n: int, world: int):
@@ -73,8 +79,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=0, help="override m=n=k")
-    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--config", choices=["auto", "c2", "c3", "c4", "c5"], default="auto")
+    ap.add_argument("--n", type=int, default=0, help="override m=n=k (c2/c3/c5)")
+    ap.add_argument("--dtype", choices=["f64", "f32", "bf16", "f16"], default=None)
     ap.add_argument("--nb", type=int, default=128, help="El::Blocksize (communication panel)")
     ap.add_argument("--kc", type=int, default=0, help="compute panel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -101,14 +108,32 @@ def main():
     else:
         comm = el.Comm.self_comm()
     grid = el.Grid(comm, 0)
-    n = args.n or (32768 if world == 1 else 65536)
-    dt = el.F64 if args.dtype == "f64" else el.F32
+    gshape = f"{grid.height}x{grid.width}"
+
+    config = args.config if args.config != "auto" else ("c2" if world == 1 else "c3")
+    dtype = args.dtype or {"c2": "f64", "c3": "f64", "c4": "f32", "c5": "bf16"}[config]
+    DT = {"f64": el.F64, "f32": el.F32, "bf16": el.BF16, "f16": el.F16}[dtype]
     el.SetBlocksize(args.nb)
     el.SetComputePanel(args.kc)
-
-    A = el.DistMatrix(grid, dt, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(1, 0.0, 0.1)
-    B = el.DistMatrix(grid, dt, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(2, 0.0, 0.1)
-    C = el.DistMatrix(grid, dt, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(3, 0.0, 0.1)
+    scaling = "strong"
+    if config == "c4":
+        m = n = 8192
+        k = 524288 * world
+        oA = el.TRANSPOSE
+        # A is k x m and B is k x n, both [VC,STAR] (k over all ranks, LBANN-native)
+        A = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
+        scaling = "weak"
+        workload = f"C4: El::Gemm TN {dtype} m=n=8192 k={k} (SUMMA_DOT), A,B [VC,STAR], Grid {gshape}"
+    else:
+        m = n = k = args.n or {"c2": 32768, "c3": 65536, "c5": 32768}[config]
+        oA = el.NORMAL
+        A = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=k).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
+        workload = (f"C2: El::Gemm NN {dtype} m=n=k={m}, Grid {gshape}" if config == "c2" else
+                    f"C3: SUMMA El::Gemm NN {dtype} m=n=k={m}, Grid {gshape}" if config == "c3" else
+                    f"C5: SUMMA El::Gemm NN {dtype} m=n=k={m} + DistMatrix Axpy/Hadamard, Grid {gshape}")
+    C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=n).fill_hash(3, 0.0, 0.1)
 
     def barrier():
         el.device_synchronize()
@@ -117,7 +142,7 @@ def main():
             dist.barrier()
 
     def step():
-        return el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
+        return el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
 
     for _ in range(args.warmup):
         step()
@@ -132,26 +157,28 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    import ctypes
     gemm_ms, launches, flops = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
     comm_ms, comm_bytes = ctypes.c_double(), ctypes.c_int64()
     L.call("elx_profile_stats", ctypes.byref(gemm_ms), ctypes.byref(launches), ctypes.byref(flops),
            ctypes.byref(comm_ms), ctypes.byref(comm_bytes))
     L.call("elx_set_profiling", 0)
 
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
 
-    total_flops = 2.0 * n * n * n * args.steps
+    elapsed = max_over_ranks(elapsed)
+    total_flops = 2.0 * m * n * k * args.steps
     value = total_flops / elapsed / 1e12
     avg_ms = gemm_ms.value / max(launches.value, 1)
     flops_per_launch = flops.value / max(launches.value, 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    peak = PEAK_TFLOPS[args.dtype]
+    peak = PEAK_TFLOPS[dtype]
     out = {
-        "metric": "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "TFLOP/s",
         "n_gpus": world,
@@ -159,29 +186,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": scaling,
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": dtype,
         "data": "synthetic (grid-independent hash, Uniform(-0.1,0.1)); alpha=0.5, beta=-0.5",
         "config": {
-            "workload": ("C2: El::Gemm NN fp64 m=n=k=32768, Grid 1x1" if world == 1 and n == 32768 else
-                         f"C3: SUMMA El::Gemm NN {args.dtype} m=n=k={n}, Grid {grid.height}x{grid.width}"),
-            "m": n, "n": n, "k": n,
-            "grid": f"{grid.height}x{grid.width}",
+            "workload": workload,
+            "m": m, "n": n, "k": k,
+            "grid": gshape,
             "algorithm": {2: "SUMMA_A", 4: "SUMMA_B", 6: "SUMMA_C", 7: "SUMMA_DOT"}.get(alg, str(alg)),
             "blocksize": args.nb,
             "compute_panel": args.kc or "auto",
-            "parallelism": f"grid{grid.height}x{grid.width}",
+            "parallelism": f"grid{gshape}",
         },
         "pct_of_mfma_peak": round(100.0 * value / (peak * world), 2),
         "roofline": {
             "bound": "mfma",
-            "kernel": f"gemm_tile_kernel<{'double' if args.dtype == 'f64' else 'float'}> (local panel update)",
+            "kernel": f"{KERNEL[dtype]} (local panel update)",
             "achieved": round(achieved, 3),
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "traffic": measured_traffic(args.dtype, n, world),
+            "traffic": measured_traffic(dtype, m, world) if config in ("c2", "c3") else None,
             "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
             "launches_timed": launches.value,
             "avg_launch_ms": round(avg_ms, 3),
@@ -193,6 +219,24 @@ def main():
             "GB_per_s": round(comm_bytes.value / (comm_ms.value * 1e-3) / 1e9, 2) if comm_ms.value > 0 else None,
         },
     }
+    if config == "c5":
+        # DistMatrix Axpy / Hadamard on the [MC,MR] operands (no exchange: each
+        # rank updates its local block); HBM bytes 3 x local elements x size
+        es = {"f64": 8, "f32": 4, "bf16": 2, "f16": 2}[dtype]
+        loc = A.LocalHeight() * A.LocalWidth()
+        ew = {}
+        for name, fn, reps in (("axpy", lambda: el.Axpy(0.5, A, C), 20), ("hadamard", lambda: el.Hadamard(A, B, C), 20)):
+            fn()
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            barrier()
+            dt = max_over_ranks((time.perf_counter() - t1) / reps)
+            gbs = 3 * es * loc / dt / 1e9
+            ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
+                        "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+        out["entrywise"] = ew
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -66,6 +66,11 @@ def lib():
                                         c_void_p, i64]
         L.orc_fro.restype = d
         L.orc_fro.argtypes = [i64, i64, c_void_p, i64]
+        L.orc_cpu_gemm_f64.restype = None
+        L.orc_cpu_gemm_f64.argtypes = [c_char, c_char, i64, i64, i64, d, c_void_p, i64, c_void_p, i64, d,
+                                       c_void_p, i64]
+        L.orc_cpu_threads.restype = c_int
+        L.orc_cpu_threads.argtypes = []
         _lib = L
     return _lib
 
@@ -143,6 +148,22 @@ def gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndar
     f(ta.encode(), tb.encode(), m, n, k, alpha, _p(A), max(A.shape[0], 1), _p(B), max(B.shape[0], 1), beta,
       _p(C), max(m, 1))
     return C
+
+
+def cpu_gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """bench.py's CPU baseline: blocked OpenMP f64 GEMM (cpu_gemm.c), BLAS semantics."""
+    C = np.array(C, order="F", copy=True, dtype=np.float64)
+    A = np.asfortranarray(A, dtype=np.float64)
+    B = np.asfortranarray(B, dtype=np.float64)
+    m, n = C.shape
+    k = A.shape[1] if ta == "N" else A.shape[0]
+    lib().orc_cpu_gemm_f64(ta.encode(), tb.encode(), m, n, k, alpha, _p(A), max(A.shape[0], 1), _p(B),
+                           max(B.shape[0], 1), beta, _p(C), max(m, 1))
+    return C
+
+
+def cpu_threads() -> int:
+    return int(lib().orc_cpu_threads())
 
 
 def gemm_half(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:

@@ -52,6 +52,13 @@ void orc_gemm_f32(char ta, char tb, int64_t m, int64_t n, int64_t k, float alpha
 void orc_summa_nnc_f64(int r, int c, int64_t m, int64_t n, int64_t k, int64_t nb, double alpha, const double* A,
                        int64_t lda, const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
 
+/* bench.py's CPU baseline (cpu_gemm.c): blocked, packed, OpenMP-parallel
+ * BLAS-semantics dgemm standing in for the reference's multi-threaded BLAS
+ * call (src/core/imports/blas/Gemm.hpp:13-40) */
+void orc_cpu_gemm_f64(char ta, char tb, int64_t m, int64_t n, int64_t k, double alpha, const double* A, int64_t lda,
+                      const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
+int orc_cpu_threads(void);
+
 /* parity metric of the north_star: ||C - Cref||_F / (||A||_F ||B||_F k eps) */
 double orc_fro(int64_t m, int64_t n, const double* X, int64_t ldx);
 
