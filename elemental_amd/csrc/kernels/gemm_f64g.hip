@@ -1,0 +1,210 @@
+// fp64 local panel update, LDS-DMA path for gfx950: C := alpha op(A) op(B) + beta C
+// (column-major).  The hot kernel of configs C1-C3 (SUMMA's LocalGemm,
+// src/blas_like/level3/Gemm.cpp:163-186 -> rocblas_dgemm in the reference,
+// include/hydrogen/blas/GPU_BLAS_impl.hpp:397-423).
+//
+// Why a second fp64 kernel: ablating the register-staged kernel of
+// gemm_mfma.hip (profiles/r01_sched_knobs.log) showed the slab staging
+// (global_load -> VGPR -> select -> ds_write) costs ~12 % of the MFMA pipe,
+// the barriers ~3 %.  Here the staging is global_load_lds (LDS DMA): no VGPR
+// round trip, no ds_write issue, no selects, and the next slab is in flight
+// across the MFMAs of the current one.
+//
+// Geometry: 128 x 128 tile, BK = 16, 8 waves of 32 x 64 (2 x 4 accumulators of
+// v_mfma_f64_16x16x4_f64), two LDS stages of 32 KiB -> two workgroups per CU
+// (4 waves per SIMD).  LDS images, 16-B chunk XOR swizzles applied to the
+// glds SOURCE addresses (the DMA writes lane-linearly), conflict-free reads:
+//   KC (k contiguous in HBM): [128 rows][16 k] (128-B rows), chunk c -> c ^ ((r>>1)&7)
+//   RC (rows contiguous):     [16 k][128 rows] (1-KiB k-rows), chunk c -> c ^ 8(kk&1)
+// Edges: rows past m/n are clamped (read, never stored); k is a multiple of 16
+// here (the k tail goes to the general kernel); 16-B aligned operands.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.hpp"
+
+namespace elx {
+namespace kern {
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_char;
+
+constexpr int BM = 128, BN = 128, BK = 16, NT = 512, GROUP_M = 8;
+constexpr int IMG = 128 * BK * 8;  // one operand image: 16 KiB
+constexpr int STAGE = 2 * IMG;     // A image then B image
+
+struct GParams {
+    i64 m, n, k;  // k: multiple of BK
+    double alpha, beta;
+    const double* A; i64 lda;
+    const double* B; i64 ldb;
+    double* C; i64 ldc;
+    int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int per_group = GROUP_M * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int inner = wg - group * per_group;
+    tm = first_m + inner % gsz;
+    tn = inner / gsz;
+}
+
+__device__ __forceinline__ void glds16(const double* src, lds_char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// Stage one operand image (128 operand rows from global row R, 16 k from k0):
+// 16 wave-instructions of 1 KiB, wave w issues w and w + 8.
+template <bool KC>
+__device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
+                                          int l) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ins = w + 8 * q;
+        if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
+            const int r = ins * 8 + (l >> 3);
+            const int c = (l & 7) ^ ((r >> 1) & 7);
+            i64 row = R + r;
+            row = row < rows ? row : rows - 1;
+            glds16(X + row * ld + k0 + 2 * c, img + ins * 1024);
+        } else {   // X(row, k) = X[row + k*ld]; one 1-KiB k-row per instruction
+            const int kk = ins;
+            const int c = l ^ ((kk & 1) << 3);
+            i64 col = R + 2 * c;
+            col = col <= rows - 2 ? col : rows - 2;
+            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+        }
+    }
+}
+
+// Operand of one 16x16x4 MFMA: lane l holds X(R0 + (l&15), 4s + (l>>4)).
+template <bool KC>
+__device__ __forceinline__ double opnd(const lds_char* img, int R0, int s, int l) {
+    const int r = R0 + (l & 15), k = 4 * s + (l >> 4);
+    int off;
+    if (KC) off = r * 128 + ((((k >> 1) ^ ((r >> 1) & 7))) << 4) + ((k & 1) << 3);
+    else off = k * 1024 + ((((r >> 1) ^ ((k & 1) << 3))) << 4) + ((r & 1) << 3);
+    return *(const __attribute__((address_space(3))) double*)(img + off);
+}
+
+struct Frame {
+    const double* A; i64 lda, m, m0;
+    const double* B; i64 ldb, n, n0;
+    int w, l, wr, wc;
+};
+
+// One slab: stage slab t+1 into `next` and run slab t's MFMAs from `cur`.  The
+// __restrict__ LDS pointers give the inlined accesses alias scopes, so the
+// waitcnt pass does not drain the in-flight DMA before the ds_reads.
+template <bool KCA, bool KCB>
+__device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
+                                     const lds_char* __restrict__ cur, f64x4 (&acc)[2][4]) {
+    if (more) {
+        stage_img<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+    }
+    const lds_char* Ai = cur;
+    const lds_char* Bi = cur + IMG;
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+        double a[2], b[4];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) a[mi] = opnd<KCA>(Ai, f.wr * 32 + mi * 16, s, f.l);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB>(Bi, f.wc * 64 + ni * 16, s, f.l);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    }
+}
+
+template <bool KCA, bool KCB, bool BETA0>
+__global__ __launch_bounds__(NT, 2) void gemm_f64g_kernel(GParams p) {
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;  // 4 (M) x 2 (N) waves of 32 x 64
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f64x4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    stage_img<KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        slab<KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
+        __syncthreads();                                   // and every wave is done with this one
+    }
+
+    // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
+    const int g = l >> 4, c = l & 15;
+    const i64 ib = m0 + wr * 32, jb = n0 + wc * 64;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const i64 j = jb + ni * 16 + c;
+            if (j >= p.n) continue;
+            double* col = p.C + j * p.ldc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const i64 i = ib + mi * 16 + g + 4 * r;
+                if (i < p.m) {
+                    const double v = p.alpha * acc[mi][ni][r];
+                    col[i] = BETA0 ? v : v + p.beta * col[i];
+                }
+            }
+        }
+}
+
+template <bool KCA, bool KCB>
+hipError_t launch_g(const GParams& p, hipStream_t s) {
+    const dim3 grid(p.tiles_m * p.tiles_n);
+    if (p.beta == 0.0) hipLaunchKernelGGL((gemm_f64g_kernel<KCA, KCB, true>), grid, dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f64g_kernel<KCA, KCB, false>), grid, dim3(NT), 0, s, p);
+    return hipGetLastError();
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+}  // namespace
+
+bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B, i64 ldb) {
+    const bool kca = ta, kcb = !tb;
+    return k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
+           (kcb || (n % 2 == 0 && n >= 2)) && ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 512 &&
+           m < (1ll << 31) && n < (1ll << 31);
+}
+
+// C = alpha op(A)(:, :kmain) op(B)(:kmain, :) + beta C over the k16 = k / 16 * 16 prefix;
+// the caller adds the k tail.
+hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
+                            const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
+    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN)};
+    const bool kca = ta, kcb = !tb;
+    if (kca) return kcb ? launch_g<true, true>(p, s) : launch_g<true, false>(p, s);
+    return kcb ? launch_g<false, true>(p, s) : launch_g<false, false>(p, s);
+}
+
+}  // namespace kern
+}  // namespace elx

@@ -30,6 +30,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <algorithm>
+#include <string>
+#include "kernels.hpp"
 
 namespace elx {
 namespace kern {
@@ -438,9 +440,32 @@ static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
     return launch_split<T, Tile128, TA, TB, false, false>(p, s);
 }
 
+// fp64 kernel choice: "dma" (default) = gemm_f64g.hip, LDS-DMA staging, 70.9 TF
+// at 16384^3 vs 65.9 for "reg" = the register-staged tile kernel here
+// (tools/f64_ab.py, profiles/r01_f64_ab.log); ELX_F64_KERNEL=reg|dma overrides.
+static bool f64_use_dma() {
+    static const bool dma = [] {
+        const char* v = getenv("ELX_F64_KERNEL");
+        return v ? std::string(v) != "reg" : true;
+    }();
+    return dma;
+}
+
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s) {
+    if constexpr (sizeof(T) == 8) {
+        if (f64_use_dma() && gemm_f64_lds_dma_ok(ta, tb, m, n, k, A, lda, B, ldb)) {
+            const i64 k16 = k / 16 * 16;
+            hipError_t e = gemm_f64_lds_dma(ta, tb, m, n, k16, alpha, A, lda, B, ldb, beta, C, ldc, s);
+            if (e != hipSuccess || k16 == k) return e;
+            // k tail: C += alpha op(A)(:, k16:) op(B)(k16:, :)
+            A += ta ? k16 : k16 * lda;
+            B += tb ? k16 * ldb : k16;
+            k -= k16;
+            beta = T(1);
+        }
+    }
     GemmParams<T> p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0, std::max<i64>(k, 1), 0};
     if (ta) return tb ? launch_tn<T, true, true>(p, s) : launch_tn<T, true, false>(p, s);
     return tb ? launch_tn<T, false, true>(p, s) : launch_tn<T, false, false>(p, s);

@@ -11,6 +11,11 @@ using i64 = int64_t;
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s);
+// fp64 LDS-DMA kernel (gemm_f64g.hip): k16 multiple of 16, the caller adds the tail
+bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B,
+                         i64 ldb);
+hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
+                            const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s);
 // 16-bit GEMMs: is_bf16 selects bf16 vs f16 storage; f32 accumulation.
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
                        const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,

@@ -39,6 +39,8 @@ OPS = {"N": L.NORMAL, "T": L.TRANSPOSE}
 SHAPES = [(1, 1, 1), (67, 53, 41), (128, 128, 16), (255, 257, 130), (300, 200, 517), (16, 700, 3),
           # few output tiles, long k: split-k chunks + ordered reduce (even and odd k)
           (96, 80, 9000), (67, 53, 4099)]
+# >= 512 128x128 tiles: the fp64 LDS-DMA kernel (ragged edges, k tail of 4)
+BIG = [(3000, 2900, 100)]
 
 
 @pytest.mark.parametrize("dt", ["f64", "f32"])
@@ -48,7 +50,7 @@ def test_local_gemm_f64_f32(dt, ta, tb):
     npdt = np.float64 if dt == "f64" else np.float32
     eps = np.finfo(npdt).eps
     fn = L.lib().elx_gemm_f64 if dt == "f64" else L.lib().elx_gemm_f32
-    for (m, n, k) in SHAPES:
+    for (m, n, k) in SHAPES + BIG:
         for beta in (0.0, -0.5):
             A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 11, 0, 1, npdt)
             B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, 12, 0, 1, npdt)
