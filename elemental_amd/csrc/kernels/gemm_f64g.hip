@@ -20,6 +20,7 @@
 // here (the k tail goes to the general kernel); 16-B aligned operands.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "kernels.hpp"
 
 namespace elx {
@@ -30,9 +31,15 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 
-constexpr int BM = 128, BN = 128, BK = 16, NT = 512, GROUP_M = 8;
-constexpr int IMG = 128 * BK * 8;  // one operand image: 16 KiB
-constexpr int STAGE = 2 * IMG;     // A image then B image
+constexpr int BN = 128, BK = 16, GROUP_M = 8;
+// Tile shapes: BM = 128 (8 waves, 2 workgroups per CU) or 256 (16 waves, one
+// workgroup per CU, 25 % fewer staged bytes per FLOP); waves are 32 x 64 each.
+template <int BM_>
+struct Shape {
+    static constexpr int BM = BM_, WM = BM_ / 32, NW = 2 * WM, NT = 64 * NW;
+    static constexpr int IMGA = BM * BK * 8, IMGB = BN * BK * 8, STAGE = IMGA + IMGB;
+    static constexpr int MINB = BM == 128 ? 2 : 1;
+};
 
 struct GParams {
     i64 m, n, k;  // k: multiple of BK
@@ -59,23 +66,25 @@ __device__ __forceinline__ void glds16(const double* src, lds_char* dst) {
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-// Stage one operand image (128 operand rows from global row R, 16 k from k0):
-// 16 wave-instructions of 1 KiB, wave w issues w and w + 8.
-template <bool KC>
+// Stage one operand image (ROWS operand rows from global row R, 16 k from k0):
+// ROWS/8 wave-instructions of 1 KiB dealt over NW waves.
+template <bool KC, int ROWS, int NW>
 __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
+    constexpr int NINS = ROWS * BK * 8 / 1024;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ins = w + 8 * q;
+    for (int q = 0; q < NINS / NW; ++q) {
+        const int ins = w + NW * q;
         if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
             const int r = ins * 8 + (l >> 3);
             const int c = (l & 7) ^ ((r >> 1) & 7);
             i64 row = R + r;
             row = row < rows ? row : rows - 1;
             glds16(X + row * ld + k0 + 2 * c, img + ins * 1024);
-        } else {   // X(row, k) = X[row + k*ld]; one 1-KiB k-row per instruction
-            const int kk = ins;
-            const int c = l ^ ((kk & 1) << 3);
+        } else {   // X(row, k) = X[row + k*ld]; k-rows of ROWS*8 B, 1 KiB per instruction
+            constexpr int IPR = ROWS * 8 / 1024;  // instructions per k-row
+            const int kk = ins / IPR;
+            const int c = ((ins % IPR) * 64 + l) ^ ((kk & 1) << 3);
             i64 col = R + 2 * c;
             col = col <= rows - 2 ? col : rows - 2;
             glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
@@ -84,12 +93,12 @@ __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64
 }
 
 // Operand of one 16x16x4 MFMA: lane l holds X(R0 + (l&15), 4s + (l>>4)).
-template <bool KC>
+template <bool KC, int ROWS>
 __device__ __forceinline__ double opnd(const lds_char* img, int R0, int s, int l) {
     const int r = R0 + (l & 15), k = 4 * s + (l >> 4);
     int off;
     if (KC) off = r * 128 + ((((k >> 1) ^ ((r >> 1) & 7))) << 4) + ((k & 1) << 3);
-    else off = k * 1024 + ((((r >> 1) ^ ((k & 1) << 3))) << 4) + ((r & 1) << 3);
+    else off = k * (ROWS * 8) + ((((r >> 1) ^ ((k & 1) << 3))) << 4) + ((r & 1) << 3);
     return *(const __attribute__((address_space(3))) double*)(img + off);
 }
 
@@ -102,22 +111,22 @@ struct Frame {
 // One slab: stage slab t+1 into `next` and run slab t's MFMAs from `cur`.  The
 // __restrict__ LDS pointers give the inlined accesses alias scopes, so the
 // waitcnt pass does not drain the in-flight DMA before the ds_reads.
-template <bool KCA, bool KCB>
+template <typename SH, bool KCA, bool KCB>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
                                      const lds_char* __restrict__ cur, f64x4 (&acc)[2][4]) {
     if (more) {
-        stage_img<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+        stage_img<KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<KCB, BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
     }
     const lds_char* Ai = cur;
-    const lds_char* Bi = cur + IMG;
+    const lds_char* Bi = cur + SH::IMGA;
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
         double a[2], b[4];
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) a[mi] = opnd<KCA>(Ai, f.wr * 32 + mi * 16, s, f.l);
+        for (int mi = 0; mi < 2; ++mi) a[mi] = opnd<KCA, SH::BM>(Ai, f.wr * 32 + mi * 16, s, f.l);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB>(Bi, f.wc * 64 + ni * 16, s, f.l);
+        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB, BN>(Bi, f.wc * 64 + ni * 16, s, f.l);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -126,13 +135,16 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
     }
 }
 
-template <bool KCA, bool KCB, bool BETA0>
-__global__ __launch_bounds__(NT, 2) void gemm_f64g_kernel(GParams p) {
+// FL: diagnostic flags (1 = no staging after the first slab, 2 = no slab barrier:
+// timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7)
+template <typename SH, bool KCA, bool KCB, bool BETA0, int FL = 0>
+__global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) {
+    constexpr int BM = SH::BM, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;  // 4 (M) x 2 (N) waves of 32 x 64
+    const int wr = w >> 1, wc = w & 1;  // WM (M) x 2 (N) waves of 32 x 64
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
@@ -145,15 +157,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_f64g_kernel(GParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    stage_img<KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (FL & 4) {
+        if (w >= SH::NW / 2) __builtin_amdgcn_s_setprio(1);
+    }
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<SH, KCA, KCB>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
-        __syncthreads();                                   // and every wave is done with this one
+        if (!(FL & 2)) __syncthreads();                     // and every wave is done with this one
     }
 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
@@ -177,12 +192,25 @@ __global__ __launch_bounds__(NT, 2) void gemm_f64g_kernel(GParams p) {
         }
 }
 
-template <bool KCA, bool KCB>
-hipError_t launch_g(const GParams& p, hipStream_t s) {
+template <typename SH, bool KCA, bool KCB>
+hipError_t launch_g(GParams p, hipStream_t s) {
+    p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
     const dim3 grid(p.tiles_m * p.tiles_n);
-    if (p.beta == 0.0) hipLaunchKernelGGL((gemm_f64g_kernel<KCA, KCB, true>), grid, dim3(NT), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f64g_kernel<KCA, KCB, false>), grid, dim3(NT), 0, s, p);
+    static const int fl = [] { const char* v = getenv("ELX_F64G_FLAGS"); return v ? atoi(v) : 0; }();
+    if constexpr (!KCA && KCB) {
+        if (fl == 1) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 1>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 2) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 2>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 4) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 4>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
+    }
+    if (p.beta == 0.0) hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, true>), grid, dim3(SH::NT), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false>), grid, dim3(SH::NT), 0, s, p);
     return hipGetLastError();
+}
+
+template <typename SH>
+hipError_t launch_shape(bool kca, bool kcb, const GParams& p, hipStream_t s) {
+    if (kca) return kcb ? launch_g<SH, true, true>(p, s) : launch_g<SH, true, false>(p, s);
+    return kcb ? launch_g<SH, false, true>(p, s) : launch_g<SH, false, false>(p, s);
 }
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
@@ -192,7 +220,7 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B, i64 ldb) {
     const bool kca = ta, kcb = !tb;
     return k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
-           (kcb || (n % 2 == 0 && n >= 2)) && ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 512 &&
+           (kcb || (n % 2 == 0 && n >= 2)) && ((m + 127) / 128) * ((n + BN - 1) / BN) >= 512 &&
            m < (1ll << 31) && n < (1ll << 31);
 }
 
@@ -200,10 +228,10 @@ bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A,
 // the caller adds the k tail.
 hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
                             const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
-    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN)};
-    const bool kca = ta, kcb = !tb;
-    if (kca) return kcb ? launch_g<true, true>(p, s) : launch_g<true, false>(p, s);
-    return kcb ? launch_g<false, true>(p, s) : launch_g<false, false>(p, s);
+    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN)};
+    static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();
+    if (bm == 256) return launch_shape<Shape<256>>(ta, !tb, p, s);
+    return launch_shape<Shape<128>>(ta, !tb, p, s);
 }
 
 }  // namespace kern

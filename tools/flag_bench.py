@@ -20,5 +20,7 @@ for (m, n, k) in [(16384, 16384, 16384), (32768, 16384, 4096), (32768, 32768, 81
     del A, B, C
 '''
 for f in sys.argv[1:] or ["0", "1", "2", "3", "4", "5", "7"]:
-    env = dict(os.environ, ELX_GEMM_FLAGS=f)
+    env = dict(os.environ, ELX_GEMM_FLAGS=f, ELX_F64G_FLAGS=f.split(":")[0])
+    if ":" in f:
+        env["ELX_F64G_BM"] = f.split(":")[1]
     subprocess.run([sys.executable, "-c", code % (ROOT, f)], env=env, check=True)
