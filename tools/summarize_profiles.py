@@ -5,6 +5,7 @@ correction in MI355X_MICROARCH.md §HBM, + WRITE_SIZE; both in KB)."""
 import csv, glob, json, os, shutil, sys
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 key = sys.argv[2] if len(sys.argv) > 2 else "f64:32768:1"  # dtype:n:n_gpus of the profiled bench command
+kpat = sys.argv[3] if len(sys.argv) > 3 else "gemm_f64g_kernel"  # the dominant kernel's name fragment
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "gpurun_out")
 prof = os.path.join(root, "profiles")
@@ -15,7 +16,7 @@ if stats:
 res = {"kernel": None, "counters": {}}
 for d in sorted(glob.glob(os.path.join(out, f"prof_{tag}_pmc*"))):
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
-        rows = [r for r in csv.DictReader(open(f)) if "gemm_tile_kernel" in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(f)) if kpat in r["Kernel_Name"]]
         if not rows:
             continue
         res["kernel"] = rows[0]["Kernel_Name"]
