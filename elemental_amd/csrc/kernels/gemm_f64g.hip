@@ -48,15 +48,18 @@ struct GParams {
     const double* B; i64 ldb;
     double* C; i64 ldc;
     int tiles_m, tiles_n;
+    int group_m;  // tile-order group height (L2 locality of the concurrently running tiles)
+    int xcd_remap;
 };
 
-__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int remap, int& tm,
+                                        int& tn) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int per_group = GROUP_M * tiles_n;
+    const int wg = remap ? (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3) : bid;
+    const int per_group = group_m * tiles_n;
     const int group = wg / per_group;
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int first_m = group * group_m;
+    const int gsz = min(tiles_m - first_m, group_m);
     const int inner = wg - group * per_group;
     tm = first_m + inner % gsz;
     tn = inner / gsz;
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) 
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 1, wc = w & 1;  // WM (M) x 2 (N) waves of 32 x 64
     int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
@@ -228,7 +231,9 @@ bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A,
 // the caller adds the k tail.
 hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
                             const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
-    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN)};
+    static const int gm = [] { const char* v = getenv("ELX_F64G_GROUP"); return v ? atoi(v) : GROUP_M; }();
+    static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
+    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), gm, rm};
     static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();
     if (bm == 256) return launch_shape<Shape<256>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);
