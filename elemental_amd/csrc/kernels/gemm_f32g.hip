@@ -1,0 +1,227 @@
+// fp32 local panel update, LDS-DMA path for gfx950: C := alpha op(A) op(B) + beta C
+// (column-major).  Replaces rocblas_sgemm on the hot path (configs C3-fp32 and
+// C4: src/hydrogen/device/rocBLAS_API.cpp:151-170 via GPU_BLAS_impl.hpp:397-423).
+//
+// Same skeleton as gemm_f64g.hip (128 x 128 tile, 8 waves of 32 x 64, two
+// LDS-DMA stages, two workgroups per CU) with fp32 specifics:
+//  * v_mfma_f32_16x16x4_f32 (exact f32, 32 cycles); BK = 32 so a k-contiguous
+//    image row is again 128 B.
+//  * k-permuted MFMA steps: in step s (0..7) lane group g = lane>>4 supplies
+//    k = 8g + s (the same permutation for A and B, so every k of the slab is
+//    summed exactly once).  A lane then needs 8 CONSECUTIVE k of its row for
+//    the whole slab: for a k-contiguous (KC) operand that is two ds_read_b128
+//    per slab instead of eight ds_read_b32.
+//  * swizzles (16-B chunk index): KC rows c ^ ((r>>1)&5) — searched
+//    exhaustively to make both b128 reads of all four lane groups
+//    conflict-free; RC (rows contiguous, 512-B k-rows) c ^ 4((kk>>3)&1) — the two
+//    k-rows a 32-lane half of a ds_read_b32 touches land in different 64-B halves.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.hpp"
+
+namespace elx {
+namespace kern {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_char;
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 512, NW = 8, GROUP_M = 8;
+constexpr int IMG = 128 * BK * 4;  // 16 KiB per operand image
+constexpr int STAGE = 2 * IMG;
+
+struct FParams {
+    i64 m, n, k;  // k: multiple of BK
+    float alpha, beta;
+    const float* A; i64 lda;
+    const float* B; i64 ldb;
+    float* C; i64 ldc;
+    int tiles_m, tiles_n;
+    // split-k (gridDim.y chunks): chunk z covers k in [z*kchunk, min(k, (z+1)*kchunk))
+    // and writes C + z*zstride (the caller passes a workspace, alpha = 1, beta = 0)
+    i64 kchunk, zstride;
+};
+
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int per_group = GROUP_M * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int inner = wg - group * per_group;
+    tm = first_m + inner % gsz;
+    tn = inner / gsz;
+}
+
+__device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 5; }
+__device__ __forceinline__ int swz_rc(int kk) { return ((kk >> 3) & 1) << 2; }
+
+__device__ __forceinline__ void glds16(const float* src, lds_char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// 16 wave-instructions of 1 KiB per image; wave w issues w and w + 8.
+template <bool KC>
+__device__ __forceinline__ void stage_img(const float* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
+                                          int l) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ins = w + NW * q;
+        if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
+            const int r = ins * 8 + (l >> 3);
+            const int c = (l & 7) ^ swz_kc(r);
+            i64 row = R + r;
+            row = row < rows ? row : rows - 1;
+            glds16(X + row * ld + k0 + 4 * c, img + ins * 1024);
+        } else {   // X(row, k) = X[row + k*ld]; 2 k-rows of 512 B per instruction
+            const int kk = ins * 2 + (l >> 5);
+            const int c = (l & 31) ^ swz_rc(kk);
+            i64 col = R + 4 * c;
+            col = col <= rows - 4 ? col : rows - 4;
+            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+        }
+    }
+}
+
+// The slab's 8 operand values of one 16-row fragment: element s = X(R0 + (l&15), 8(l>>4) + s).
+template <bool KC>
+__device__ __forceinline__ void frag(const lds_char* img, int R0, int l, float (&v)[8]) {
+    const int r = R0 + (l & 15), g = l >> 4;
+    if (KC) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 2 * g + h;
+            const f32x4 x = *(const __attribute__((address_space(3))) f32x4*)(img + r * 128 + ((c ^ swz_kc(r)) << 4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[4 * h + e] = x[e];
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int kk = 8 * g + s;
+            const int off = kk * 512 + (((r >> 2) ^ swz_rc(kk)) << 4) + ((r & 3) << 2);
+            v[s] = *(const __attribute__((address_space(3))) float*)(img + off);
+        }
+    }
+}
+
+struct Frame {
+    const float* A; i64 lda, m, m0;
+    const float* B; i64 ldb, n, n0;
+    int w, l, wr, wc;
+};
+
+// __restrict__ LDS pointers: alias scopes so the in-flight DMA is not drained
+// before the ds_reads (see gemm_h256.hip).
+template <bool KCA, bool KCB>
+__device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
+                                     const lds_char* __restrict__ cur, f32x4 (&acc)[2][4]) {
+    if (more) {
+        stage_img<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+    }
+    float a[2][8], b[4][8];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) frag<KCA>(cur, f.wr * 32 + mi * 16, f.l, a[mi]);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) frag<KCB>(cur + IMG, f.wc * 64 + ni * 16, f.l, b[ni]);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi][s], b[ni][s], acc[mi][ni], 0, 0, 0);
+}
+
+template <bool KCA, bool KCB, bool BETA0>
+__global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;  // 4 (M) x 2 (N) waves of 32 x 64
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    {
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += KCA ? kz0 : kz0 * p.lda;
+        p.B += KCB ? kz0 : kz0 * p.ldb;
+        p.C += (i64)blockIdx.y * p.zstride;
+    }
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    stage_img<KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        slab<KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
+    const int g = l >> 4, c = l & 15;
+    const i64 ib = m0 + wr * 32 + 4 * g, jb = n0 + wc * 64 + c;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const i64 j = jb + ni * 16;
+            if (j >= p.n) continue;
+            float* col = p.C + j * p.ldc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const i64 i = ib + mi * 16 + r;
+                if (i < p.m) {
+                    const float v = p.alpha * acc[mi][ni][r];
+                    col[i] = BETA0 ? v : v + p.beta * col[i];
+                }
+            }
+        }
+}
+
+template <bool KCA, bool KCB>
+hipError_t launch_f(const FParams& p, hipStream_t s) {
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
+    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, true>), grid, dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, false>), grid, dim3(NT), 0, s, p);
+    return hipGetLastError();
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+}  // namespace
+
+DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float* A, i64 lda, const float* B,
+                              i64 ldb) {
+    const bool kca = ta, kcb = !tb;
+    const bool ok = k >= BK && al16(A) && al16(B) && lda % 4 == 0 && ldb % 4 == 0 && (kca || (m % 4 == 0 && m >= 4)) &&
+                    (kcb || (n % 4 == 0 && n >= 4)) && m < (1ll << 31) && n < (1ll << 31);
+    return dma_plan(ok, (m + BM - 1) / BM * ((n + BN - 1) / BN), k, BK);
+}
+
+hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
+                            i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s) {
+    FParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
+              kchunk, m * n};
+    const bool kca = ta, kcb = !tb;
+    if (kca) return kcb ? launch_f<true, true>(p, s) : launch_f<true, false>(p, s);
+    return kcb ? launch_f<false, true>(p, s) : launch_f<false, false>(p, s);
+}
+
+}  // namespace kern
+}  // namespace elx

@@ -48,6 +48,9 @@ struct GParams {
     const double* B; i64 ldb;
     double* C; i64 ldc;
     int tiles_m, tiles_n;
+    // split-k (gridDim.y chunks): chunk z covers k in [z*kchunk, min(k, (z+1)*kchunk))
+    // and writes C + z*zstride (the caller passes a workspace, alpha = 1, beta = 0)
+    i64 kchunk, zstride;
     int group_m;  // tile-order group height (L2 locality of the concurrently running tiles)
     int xcd_remap;
 };
@@ -151,6 +154,13 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) 
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    {
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += KCA ? kz0 : kz0 * p.lda;
+        p.B += KCB ? kz0 : kz0 * p.ldb;
+        p.C += (i64)blockIdx.y * p.zstride;
+    }
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
     f64x4 acc[2][4];
@@ -198,7 +208,7 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) 
 template <typename SH, bool KCA, bool KCB>
 hipError_t launch_g(GParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
-    const dim3 grid(p.tiles_m * p.tiles_n);
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
     static const int fl = [] { const char* v = getenv("ELX_F64G_FLAGS"); return v ? atoi(v) : 0; }();
     if constexpr (!KCA && KCB) {
         if (fl == 1) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 1>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
@@ -220,20 +230,21 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
 }  // namespace
 
-bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B, i64 ldb) {
+DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B,
+                              i64 ldb) {
     const bool kca = ta, kcb = !tb;
-    return k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
-           (kcb || (n % 2 == 0 && n >= 2)) && ((m + 127) / 128) * ((n + BN - 1) / BN) >= 512 &&
-           m < (1ll << 31) && n < (1ll << 31);
+    const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
+                    (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
+    return dma_plan(ok, (m + 127) / 128 * ((n + BN - 1) / BN), k, BK);
 }
 
-// C = alpha op(A)(:, :kmain) op(B)(:kmain, :) + beta C over the k16 = k / 16 * 16 prefix;
-// the caller adds the k tail.
-hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
-                            const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
+// C = alpha op(A)(:, :kmain) op(B)(:kmain, :) + beta C (kmain a multiple of 16, split
+// into kchunk pieces over gridDim.y); the caller adds the k tail.
+hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, double alpha, const double* A,
+                            i64 lda, const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
     static const int gm = [] { const char* v = getenv("ELX_F64G_GROUP"); return v ? atoi(v) : GROUP_M; }();
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
-    GParams p{m, n, k16, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), gm, rm};
+    GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), kchunk, m * n, gm, rm};
     static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();
     if (bm == 256) return launch_shape<Shape<256>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);

@@ -356,6 +356,17 @@ __global__ __launch_bounds__(256) void splitk_reduce(i64 m, i64 n, int nz, T alp
     }
 }
 
+template <typename T>
+static hipError_t launch_reduce(i64 m, i64 n, int nz, T alpha, const T* W, T beta, T* C, i64 ldc, hipStream_t s) {
+    const i64 mn = m * n;
+    const int grid = (int)std::min<i64>((mn + 255) / 256, 256 * 16);
+    if (beta == T(0))
+        hipLaunchKernelGGL((splitk_reduce<T, true>), dim3(grid), dim3(256), 0, s, m, n, nz, alpha, W, beta, C, ldc);
+    else
+        hipLaunchKernelGGL((splitk_reduce<T, false>), dim3(grid), dim3(256), 0, s, m, n, nz, alpha, W, beta, C, ldc);
+    return hipGetLastError();
+}
+
 // Split k when the output tiles alone cannot fill the chip (the Dot variant's
 // 2000 x 2000 x 524288 blocks, SUMMA_*Dot): aim for two rounds of resident
 // workgroups with chunks of >= 2048.  Returns the chunk count (1 = no split).
@@ -390,17 +401,7 @@ static hipError_t launch_split(GemmParams<T> p, hipStream_t s) {
     q.kchunk = kchunk;
     q.zstride = p.m * p.n;
     e = launch_cfg<T, CFG, TA, TB, VEC, OFF32>(q, s);
-    if (e == hipSuccess) {
-        const i64 mn = p.m * p.n;
-        const int grid = (int)std::min<i64>((mn + 255) / 256, 256 * 16);
-        if (p.beta == T(0))
-            hipLaunchKernelGGL((splitk_reduce<T, true>), dim3(grid), dim3(256), 0, s, p.m, p.n, nz, p.alpha, W, p.beta,
-                               p.C, p.ldc);
-        else
-            hipLaunchKernelGGL((splitk_reduce<T, false>), dim3(grid), dim3(256), 0, s, p.m, p.n, nz, p.alpha, W, p.beta,
-                               p.C, p.ldc);
-        e = hipGetLastError();
-    }
+    if (e == hipSuccess) e = launch_reduce(p.m, p.n, nz, p.alpha, W, p.beta, p.C, p.ldc, s);
     const hipError_t f = hipFreeAsync(W, s);
     return e != hipSuccess ? e : f;
 }
@@ -451,18 +452,54 @@ static bool f64_use_dma() {
     return dma;
 }
 
+// fp32 kernel choice: "dma" = gemm_f32g.hip, "reg" = the 256x128 register-staged
+// kernel here; ELX_F32_KERNEL overrides.
+static bool f32_use_dma() {
+    static const bool dma = [] {
+        const char* v = getenv("ELX_F32_KERNEL");
+        return v ? std::string(v) != "reg" : true;
+    }();
+    return dma;
+}
+
+static DmaPlan plan_dma(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B, i64 ldb) {
+    return gemm_f64_lds_dma_plan(ta, tb, m, n, k, A, lda, B, ldb);
+}
+static DmaPlan plan_dma(bool ta, bool tb, i64 m, i64 n, i64 k, const float* A, i64 lda, const float* B, i64 ldb) {
+    return gemm_f32_lds_dma_plan(ta, tb, m, n, k, A, lda, B, ldb);
+}
+static hipError_t run_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, double alpha, const double* A,
+                          i64 lda, const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
+    return gemm_f64_lds_dma(ta, tb, m, n, kmain, kchunk, alpha, A, lda, B, ldb, beta, C, ldc, s);
+}
+static hipError_t run_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
+                          i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s) {
+    return gemm_f32_lds_dma(ta, tb, m, n, kmain, kchunk, alpha, A, lda, B, ldb, beta, C, ldc, s);
+}
+
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s) {
-    if constexpr (sizeof(T) == 8) {
-        if (f64_use_dma() && gemm_f64_lds_dma_ok(ta, tb, m, n, k, A, lda, B, ldb)) {
-            const i64 k16 = k / 16 * 16;
-            hipError_t e = gemm_f64_lds_dma(ta, tb, m, n, k16, alpha, A, lda, B, ldb, beta, C, ldc, s);
-            if (e != hipSuccess || k16 == k) return e;
-            // k tail: C += alpha op(A)(:, k16:) op(B)(k16:, :)
-            A += ta ? k16 : k16 * lda;
-            B += tb ? k16 * ldb : k16;
-            k -= k16;
+    if (sizeof(T) == 8 ? f64_use_dma() : f32_use_dma()) {
+        const DmaPlan d = plan_dma(ta, tb, m, n, k, A, lda, B, ldb);
+        if (d.use) {
+            hipError_t e;
+            if (d.nz == 1) {
+                e = run_dma(ta, tb, m, n, d.kmain, d.kmain, alpha, A, lda, B, ldb, beta, C, ldc, s);
+            } else {  // split-k: nz partials into a stream-ordered workspace, then the ordered reduce
+                T* W = nullptr;
+                e = hipMallocAsync(reinterpret_cast<void**>(&W), sizeof(T) * (size_t)m * (size_t)n * d.nz, s);
+                if (e != hipSuccess) return e;
+                e = run_dma(ta, tb, m, n, d.kmain, d.kchunk, T(1), A, lda, B, ldb, T(0), W, m, s);
+                if (e == hipSuccess) e = launch_reduce(m, n, d.nz, alpha, W, beta, C, ldc, s);
+                const hipError_t f = hipFreeAsync(W, s);
+                if (e == hipSuccess) e = f;
+            }
+            if (e != hipSuccess || d.kmain == k) return e;
+            // k tail: C += alpha op(A)(:, kmain:) op(B)(kmain:, :) with the general kernel
+            A += ta ? d.kmain : d.kmain * lda;
+            B += tb ? d.kmain * ldb : d.kmain;
+            k -= d.kmain;
             beta = T(1);
         }
     }

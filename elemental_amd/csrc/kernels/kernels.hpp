@@ -11,11 +11,44 @@ using i64 = int64_t;
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s);
-// fp64 LDS-DMA kernel (gemm_f64g.hip): k16 multiple of 16, the caller adds the tail
-bool gemm_f64_lds_dma_ok(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B,
-                         i64 ldb);
-hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 k16, double alpha, const double* A, i64 lda,
-                            const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s);
+// LDS-DMA kernels (gemm_f64g.hip / gemm_f32g.hip, 128x128 tiles, 2 workgroups per
+// CU).  The plan says whether a shape takes them and how k is cut: kmain (a
+// multiple of the slab depth; the caller adds the k - kmain tail with the
+// general kernel, beta = 1) over nz chunks of kchunk (nz > 1: split-k into a
+// workspace of nz m x n partials, alpha = 1, beta = 0, then splitk_reduce).
+struct DmaPlan {
+    bool use;
+    i64 kmain, kchunk;
+    int nz;
+};
+inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
+    DmaPlan d{false, 0, 0, 1};
+    if (!ok) return d;
+    d.kmain = k / bk * bk;
+    const i64 slots = 512;  // two workgroups per CU
+    if (tiles >= slots) {
+        d.use = true;
+        d.kchunk = d.kmain;
+        return d;
+    }
+    // few tiles: split k into chunks of >= 2048 (whole slabs) for two rounds of workgroups
+    i64 z = (2 * slots + tiles - 1) / tiles;
+    z = z < d.kmain / 2048 ? z : d.kmain / 2048;
+    z = z < 16 ? z : 16;
+    if (z < 2) return d;
+    d.use = true;
+    d.kchunk = ((d.kmain + z - 1) / z + bk - 1) / bk * bk;
+    d.nz = (int)((d.kmain + d.kchunk - 1) / d.kchunk);
+    return d;
+}
+DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B,
+                              i64 ldb);
+hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, double alpha, const double* A,
+                            i64 lda, const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s);
+DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float* A, i64 lda, const float* B,
+                              i64 ldb);
+hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
+                            i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s);
 // 16-bit GEMMs: is_bf16 selects bf16 vs f16 storage; f32 accumulation.
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
                        const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
