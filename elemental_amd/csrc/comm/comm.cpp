@@ -252,6 +252,34 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
     }
 }
 
+void Comm::SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s) {
+    const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
+    ELX_REQUIRE(dest >= 0 && dest < size_ && src >= 0 && src < size_, "SendRecv: bad peer ", dest, "/", src, " of ",
+                size_);
+    auto& st = GlobalCommStats();
+    st.calls++;
+    if (src != rank_) st.bytes += static_cast<int64_t>(bytes);
+    if (count == 0) return;
+    if (dest == rank_ && src == rank_) { CopyBytes(dev, recv, send, bytes, s); return; }
+    if (kind_ == Kind::RCCL) {
+        ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        const ncclDataType_t nt = NcclType(t);
+        CheckNccl(ncclGroupStart(), "ncclGroupStart");
+        CheckNccl(ncclSend(send, count, nt, dest, nccl_, s), "ncclSend");
+        CheckNccl(ncclRecv(recv, count, nt, src, nccl_, s), "ncclRecv");
+        CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+        return;
+    }
+    if (dev == Device::CPU) { HostCall(ELX_COLL_SENDRECV, t, send, recv, count, dest, src); return; }
+    static Staging stg;
+    char* h = static_cast<char*>(stg.Get(bytes * 2));
+    ELX_CHECK_HIP(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+    HostCall(ELX_COLL_SENDRECV, t, h, h + bytes, count, dest, src);
+    ELX_CHECK_HIP(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, s));
+    ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
 void Comm::Barrier() {
     if (size_ == 1) return;
     if (kind_ == Kind::RCCL) {

@@ -55,6 +55,9 @@ public:
     void AllToAllV(DType t, const void* send, const std::vector<Int>& scounts, const std::vector<Int>& sdispls,
                    void* recv, const std::vector<Int>& rcounts, const std::vector<Int>& rdispls, Device dev,
                    hipStream_t s);
+    // Point-to-point exchange (El::mpi::SendRecv, src/core/imports/mpi/SendRecv.hpp:9-60):
+    // send `count` elements to `dest` while receiving `count` from `src`.
+    void SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s);
     void Barrier();
 
 private:

@@ -351,6 +351,74 @@ void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMa
     Cp.Finish();
 }
 
+// ---------------------------------------------------------------------------
+// Cannon's algorithm, NN only (NN.hpp:21-104; dispatched from Gemm.cpp:284-285).
+// Square grids, width(A) a multiple of sqrt(p).  The reference runs it on the
+// CPU only (NN.hpp:30-31); here on either device: packages are contiguous
+// copies of the local blocks, the ring shifts are SendRecv over the MR (grid
+// row) and MC (grid column) communicators (RCCL on the GPU), and each step is
+// one local MFMA update with beta = 1.
+// ---------------------------------------------------------------------------
+void Cannon(double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+    const Grid& g = CPre.G();
+    if (g.Height() != g.Width()) throw LogicError("Process grid must be square for Cannon's");
+    RWProxy Cp(CPre);
+    DistMatrix& C = Cp.Get();
+    // A aligned with C's rows, B with C's columns (NN.hpp:43-48)
+    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR, C.ColAlign(), -1);
+    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR, -1, C.RowAlign());
+    const DistMatrix& A = *Ap;
+    const DistMatrix& B = *Bp;
+    const int q = g.Height();
+    if (A.Width() % q != 0) throw LogicError("For now, width(A) must be integer multiple of sqrt(p)");
+    const Device dev = C.Dev();
+    const DType t = C.Type();
+    hipStream_t s = C.Stream();
+    if (dev == Device::GPU) {
+        FenceStreams(A.Stream(), s);
+        FenceStreams(B.Stream(), s);
+    }
+    const Int lhA = A.LocalHeight(), lwA = A.LocalWidth(), lhB = B.LocalHeight(), lwB = B.LocalWidth();
+    const Int sizeA = lhA * lwA, sizeB = lhB * lwB;
+    const size_t es = DTypeSize(t);
+    Buffer pA[2], pB[2];
+    for (int i = 0; i < 2; ++i) {
+        pA[i].Reset(dev, std::max<size_t>(1, sizeA * es), s);
+        pB[i].Reset(dev, std::max<size_t>(1, sizeB * es), s);
+    }
+    // the initial packages: contiguous copies of the local blocks (NN.hpp:60-71)
+    exec::Copy2D d[2] = {{lhA, lwA, A.Buffer(), 1, A.LDim(), pA[0].data(), 1, std::max<Int>(lhA, 1)},
+                   {lhB, lwB, B.Buffer(), 1, B.LDim(), pB[0].data(), 1, std::max<Int>(lhB, 1)}};
+    for (auto& x : d)
+        if (x.m > 0 && x.n > 0) exec::Copy2DBatch(dev, t, &x, 1, false, 0.0, s);
+    const int row = g.MCRank(), col = g.MRRank();
+    int a = 0, b = 0;
+    auto shift = [&](int aTo, int aFrom, int bTo, int bFrom) {
+        g.MR().SendRecv(t, pA[a].data(), aTo, pA[a ^ 1].data(), aFrom, sizeA, dev, s);
+        g.MC().SendRecv(t, pB[b].data(), bTo, pB[b ^ 1].data(), bFrom, sizeB, dev, s);
+        a ^= 1;
+        b ^= 1;
+    };
+    // initial circular shifts so the A and B packages align (NN.hpp:73-84)
+    const Int colShiftB = B.ColShift(), rowShiftA = A.RowShift();
+    shift((int)Mod(col - colShiftB, q), (int)Mod(col + colShiftB, q), (int)Mod(row - rowShiftA, q),
+          (int)Mod(row + rowShiftA, q));
+    const int aboveRow = (int)Mod(row - 1, q), belowRow = (int)Mod(row + 1, q);
+    const int leftCol = (int)Mod(col - 1, q), rightCol = (int)Mod(col + 1, q);
+    for (int step = 0; step < q; ++step) {
+        const Int m = C.LocalHeight(), n = C.LocalWidth();
+        if (m > 0 && n > 0 && lwA > 0)
+            exec::Gemm(dev, t, false, false, m, n, lwA, alpha, pA[a].data(), std::max<Int>(lhA, 1), pB[b].data(),
+                       std::max<Int>(lhB, 1), 1.0, C.Buffer(), C.LDim(), s);
+        if (step != q - 1) shift(leftCol, rightCol, aboveRow, belowRow);
+    }
+    if (dev == Device::GPU) {
+        FenceStreams(s, A.Stream());  // the packages are freed on s; the proxies' owners may reuse A/B
+        FenceStreams(s, B.Stream());
+    }
+    Cp.Finish();
+}
+
 int Heuristic(Int m, Int n, Int k) {  // NN.hpp:583-600 (same weights in NT/TN/TT)
     const double wC = 2.0, wDot = 10.0;
     if (wDot * m <= k && wDot * n <= k) return ELX_GEMM_SUMMA_DOT;
@@ -459,8 +527,11 @@ void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B
     case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, beta, C); break;
     case ELX_GEMM_SUMMA_DOT: SummaDot(oA, oB, alpha, A, B, C, kDotBlock); break;
     case ELX_GEMM_CANNON:
-        throw UnsupportedError("GEMM_CANNON: the reference runs Cannon on the CPU only (NN.hpp:30-31); "
-                               "not part of the MI355X path");
+        // Gemm.cpp:284-285: Cannon for NN; the other orientations' SUMMA switches
+        // reject it (NT.hpp:526, TN.hpp:524, TT.hpp:435)
+        if (oA != ELX_NORMAL || oB != ELX_NORMAL) throw LogicError("Unsupported Gemm option");
+        Cannon(alpha, A, B, C);
+        break;
     default: throw LogicError(Cat("Unsupported Gemm option ", alg));
     }
     g_last_alg = alg;

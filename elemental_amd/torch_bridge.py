@@ -78,6 +78,17 @@ class GlooBridge:
                 r = _arr(recv, count * n, dtype)
                 if count:
                     r.copy_(torch.cat([o[me * count:(me + 1) * count] for o in outs]))
+            elif op == L.COLL_SENDRECV:  # send -> group rank peer, recv <- group rank peer2
+                s = _arr(send, count, dtype).clone()
+                r = _arr(recv, count, dtype)
+                if peer == me and peer2 == me:
+                    r.copy_(s)
+                elif count:
+                    tmp = torch.empty_like(s)
+                    req = dist.isend(s, dst=ranks[peer], group=pg)
+                    dist.recv(tmp, src=ranks[peer2], group=pg)
+                    req.wait()
+                    r.copy_(tmp)
             elif op == L.COLL_BCAST:
                 t = _arr(send, count, dtype)
                 tmp = t.clone()

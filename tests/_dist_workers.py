@@ -132,6 +132,71 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         raise
 
 
+def cannon_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, seed: int):
+    """Cannon_NN (src/blas_like/level3/Gemm/NN.hpp:21-104) on a square grid with
+    misaligned A, B and C (exercises the initial skew shifts), against the
+    oracle; plus the reference's error behaviour (non-NN orientation, width(A)
+    not a multiple of sqrt(p), non-square grid)."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = np.float64 if dtype == el.F64 else np.float32
+        from elemental_amd import _lib as L
+        if r != c:
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=4, width=4)
+            B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=4, width=4)
+            C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=4, width=4)
+            try:
+                el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, B, 0.0, C, el.GEMM_CANNON)
+                raise AssertionError("Cannon on a non-square grid must raise")
+            except L.LogicError:
+                pass
+            finish()
+            return
+        rng = np.random.default_rng(seed)
+        for (m, n, k) in shapes:
+            Ag = oracle.hash_matrix(m, k, seed + 1, -0.1, 0.1, npdt)
+            Bg = oracle.hash_matrix(k, n, seed + 2, -0.1, 0.1, npdt)
+            Cg = oracle.hash_matrix(m, n, seed + 3, -0.1, 0.1, npdt)
+            ref = oracle.gemm("N", "N", 0.5, Ag, Bg, -0.5, Cg)
+            # the same random alignments on every rank
+            al = [int(x) for x in rng.integers(0, r, 6)]
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device).Align(al[0], al[1])
+            B = el.DistMatrix(g, dtype, el.MC, el.MR, device).Align(al[2], al[3])
+            C = el.DistMatrix(g, dtype, el.MC, el.MR, device).Align(al[4], al[5])
+            A.Resize(m, k)
+            B.Resize(k, n)
+            C.Resize(m, n)
+            A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank, al[0], al[1]))
+            B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank, al[2], al[3]))
+            C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank, al[4], al[5]))
+            if k % r:
+                try:
+                    el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, el.GEMM_CANNON)
+                    raise AssertionError("Cannon with width(A) % sqrt(p) != 0 must raise")
+                except L.LogicError:
+                    continue
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, el.GEMM_CANNON)
+            got = C.get_local().astype(np.float64)
+            want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank, al[4], al[5]).astype(np.float64)
+            num = np.linalg.norm(got - want) if got.size else 0.0
+            den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) * k * _tol(dtype)
+            assert num <= 10 * den, f"Cannon {m}x{n}x{k} grid {r}x{c} rank {rank}: {num / den:.3g}"
+        try:  # the other orientations reject GEMM_CANNON (NT.hpp:526 etc.)
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=4, width=4)
+            C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=4, width=4)
+            el.Gemm(el.TRANSPOSE, el.NORMAL, 1.0, A, A, 0.0, C, el.GEMM_CANNON)
+            raise AssertionError("Cannon TN must raise")
+        except L.LogicError:
+            pass
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 def blas1_worker(rank: int, world: int, port: int, height: int, device: int, seed: int):
     import oracle
     el, comm = init(rank, world, port)

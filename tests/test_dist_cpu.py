@@ -44,6 +44,13 @@ def test_gemm_f32_grid_2x2():
     _spawn(W.gemm_worker, 4, 2, el.CPU, el.F32, [(17, 21, 15)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 4, 11)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (4, 2), (2, 1)])
+def test_gemm_cannon(world, height):
+    """Cannon_NN on 1x1 and 2x2 with random alignments; LogicError on a 2x1 grid,
+    for width(A) % sqrt(p) != 0 and for non-NN orientations."""
+    _spawn(W.cannon_worker, world, height, el.CPU, el.F64, [(19, 13, 24), (8, 9, 40), (5, 7, 9)], 5)
+
+
 @pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
 def test_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.CPU, 5)

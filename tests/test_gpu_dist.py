@@ -42,6 +42,13 @@ def test_gpu_summa_all_variants(world, height):
     _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 61), (16, 12, 130)], algs, 16, 3)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (4, 2)])
+def test_gpu_cannon(world, height):
+    """Cannon_NN on Device::GPU (the reference is CPU-only): skew + ring shifts
+    through Comm::SendRecv, local MFMA updates, random alignments."""
+    _spawn(W.cannon_worker, world, height, el.GPU, el.F64, [(45, 37, 62), (16, 12, 130)], 5)
+
+
 def test_gpu_summa_f32():
     _spawn(W.gemm_worker, 2, 1, el.GPU, el.F32, [(65, 33, 97)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 8, 9)
 
