@@ -142,7 +142,8 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
 }
 
 // FL: diagnostic flags (1 = no staging after the first slab, 2 = no slab barrier:
-// timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7)
+// timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7;
+// 8 = no wait for the DMA before the barrier, also wrong results)
 template <typename SH, bool KCA, bool KCB, bool BETA0, int FL = 0>
 __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) {
     constexpr int BM = SH::BM, STAGE = SH::STAGE;
@@ -180,8 +181,13 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) 
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
         slab<SH, KCA, KCB>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
-        if (!(FL & 2)) __syncthreads();                     // and every wave is done with this one
+        if (FL & 8) {  // raw barrier: no vmcnt drain (ablation only)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
+            if (!(FL & 2)) __syncthreads();                     // and every wave is done with this one
+        }
     }
 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
@@ -214,6 +220,7 @@ hipError_t launch_g(GParams p, hipStream_t s) {
         if (fl == 1) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 1>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
         if (fl == 2) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 2>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
         if (fl == 4) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 4>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 8) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 8>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
     }
     if (p.beta == 0.0) hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, true>), grid, dim3(SH::NT), 0, s, p);
     else hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false>), grid, dim3(SH::NT), 0, s, p);
