@@ -25,6 +25,7 @@ CPU, GPU = 0, 1
 F32, F64, F16, BF16 = 0, 1, 2, 3
 (MAP_IDENTITY, MAP_NEGATE, MAP_ABS, MAP_SQUARE, MAP_SQRT, MAP_EXP, MAP_LOG, MAP_RELU, MAP_SIGMOID,
  MAP_RECIP, MAP_TANH) = range(11)
+(COMBINE_ADD, COMBINE_SUB, COMBINE_MUL, COMBINE_DIV, COMBINE_MAX, COMBINE_MIN, COMBINE_RELU_GRAD) = range(7)
 COLL_ALLGATHER, COLL_REDUCE_SCATTER, COLL_ALLTOALL, COLL_SENDRECV, COLL_BCAST, COLL_ALLREDUCE, \
     COLL_BARRIER = range(7)
 
@@ -61,6 +62,7 @@ _SIGS = {
     "elx_fill2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _vp]),
     "elx_hadamard2d": (_i, [_i, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_entrywise_map": (_i, [_i, _i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "elx_combine": (_i, [_i, _i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_fill_hash": (_i, [_i, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, c_uint64, _d, _d, _vp]),
     "elx_comm_unique_id": (_i, [POINTER(c_ubyte)]),
     "elx_comm_init_rccl": (_i, [POINTER(c_void_p), _i, _i, POINTER(c_ubyte)]),
@@ -97,6 +99,7 @@ _SIGS = {
     "elx_dm_zero": (_i, [_vp]),
     "elx_dm_hadamard": (_i, [_vp, _vp, _vp]),
     "elx_dm_entrywise_map": (_i, [_i, _vp, _vp]),
+    "elx_dm_combine": (_i, [_i, _vp, _vp]),
     "elx_dm_axpy_contract": (_i, [_d, _vp, _vp]),
     "elx_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_local_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp]),

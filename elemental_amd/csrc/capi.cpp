@@ -151,6 +151,10 @@ int elx_entrywise_map(int dtype, int fn, int64_t m, int64_t n, const void* A, in
                       void* stream) {
     return Guard([&] { exec::Map(Device::GPU, ToDType(dtype), fn, m, n, A, lda, B, ldb, S(stream)); });
 }
+int elx_combine(int dtype, int fn, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb,
+                void* stream) {
+    return Guard([&] { exec::Combine(Device::GPU, ToDType(dtype), fn, m, n, A, lda, B, ldb, S(stream)); });
+}
 int elx_fill_hash(int dtype, int64_t m, int64_t n, void* A, int64_t lda, int64_t i0, int64_t istride, int64_t j0,
                   int64_t jstride, uint64_t seed, double center, double radius, void* stream) {
     return Guard([&] {
@@ -265,6 +269,7 @@ int elx_dm_scale(double alpha, elx_dm_t A) { return Guard([&] { Scale(alpha, M(A
 int elx_dm_zero(elx_dm_t A) { return Guard([&] { Zero(M(A)); }); }
 int elx_dm_hadamard(elx_dm_t A, elx_dm_t B, elx_dm_t C) { return Guard([&] { Hadamard(M(A), M(B), M(C)); }); }
 int elx_dm_entrywise_map(int fn, elx_dm_t A, elx_dm_t B) { return Guard([&] { EntrywiseMap(fn, M(A), M(B)); }); }
+int elx_dm_combine(int fn, elx_dm_t A, elx_dm_t B) { return Guard([&] { Combine(fn, M(A), M(B)); }); }
 int elx_dm_axpy_contract(double alpha, elx_dm_t A, elx_dm_t B) { return Guard([&] { AxpyContract(alpha, M(A), M(B)); }); }
 
 int elx_gemm(int oA, int oB, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C, int alg) {

@@ -192,6 +192,33 @@ void Map(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void
     });
 }
 
+template <typename Cm>
+Cm cpu_combine(int fn, Cm a, Cm b) {
+    switch (fn) {
+    case ELX_COMBINE_ADD: return a + b;
+    case ELX_COMBINE_SUB: return b - a;
+    case ELX_COMBINE_MUL: return a * b;
+    case ELX_COMBINE_DIV: return b / a;
+    case ELX_COMBINE_MAX: return a > b ? a : b;
+    case ELX_COMBINE_MIN: return a < b ? a : b;
+    case ELX_COMBINE_RELU_GRAD: return a > Cm(0) ? b : Cm(0);
+    default: throw LogicError(Cat("unknown combine functor ", fn));
+    }
+}
+
+void Combine(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s) {
+    if (fn < ELX_COMBINE_ADD || fn > ELX_COMBINE_RELU_GRAD) throw LogicError(Cat("unknown combine functor ", fn));
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) { check(kern::combine((int)t, fn, m, n, A, lda, B, ldb, s), "combine"); return; }
+    HOST_DTYPE_SWITCH(t, S, {
+        const S* a = static_cast<const S*>(A);
+        S* b = static_cast<S*>(B);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i)
+                H<S>::st(b + i + j * ldb, cpu_combine(fn, H<S>::ld(a + i + j * lda), H<S>::ld(b + i + j * ldb)));
+    });
+}
+
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

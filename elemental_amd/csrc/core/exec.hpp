@@ -21,6 +21,7 @@ void Scale(Device dev, DType t, Int m, Int n, double alpha, void* A, Int lda, hi
 void Hadamard(Device dev, DType t, Int m, Int n, const void* A, Int lda, const void* B, Int ldb,
               void* C, Int ldc, hipStream_t s);
 void Map(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s);
+void Combine(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s);
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s);
 // host-side scalar conversion of one element (for Get/Set and tests)

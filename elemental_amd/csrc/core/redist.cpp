@@ -394,4 +394,17 @@ void EntrywiseMap(int fn, const DistMatrix& A, DistMatrix& B) {  // EntrywiseMap
               B.LDim(), B.Stream());
 }
 
+void Combine(int fn, const DistMatrix& A, DistMatrix& B) {
+    if (A.Height() != B.Height() || A.Width() != B.Width())
+        throw RuntimeError("A and B must be the same size for Combine.");
+    CheckCompatible(A, B);
+    ELX_REQUIRE(A.ColDist() == B.ColDist() && A.RowDist() == B.RowDist() && A.ColAlign() == B.ColAlign() &&
+                    A.RowAlign() == B.RowAlign() && A.Dev() == B.Dev(),
+                "Combine: A and B must share distribution, alignment and device");
+    if (B.LocalHeight() == 0 || B.LocalWidth() == 0) return;
+    Fence(A, B);
+    exec::Combine(B.Dev(), B.Type(), fn, B.LocalHeight(), B.LocalWidth(), A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
+                  B.Stream());
+}
+
 }  // namespace elx

@@ -18,6 +18,9 @@ void Scale(double alpha, DistMatrix& A);
 void Zero(DistMatrix& A);
 void Hadamard(const DistMatrix& A, const DistMatrix& B, DistMatrix& C);
 void EntrywiseMap(int fn, const DistMatrix& A, DistMatrix& B);
+// B := f(A, B) on the local blocks (Combine, EntrywiseMap.hpp:187-202): same
+// size, distribution, alignment and device, else RuntimeError / LogicError
+void Combine(int fn, const DistMatrix& A, DistMatrix& B);
 
 // true iff A's local block already is B-with-B's-alignment's local block
 // (same owner of every element): lets SUMMA use views instead of copies.

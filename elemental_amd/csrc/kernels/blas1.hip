@@ -298,6 +298,32 @@ __global__ __launch_bounds__(NT) void map_kernel(i64 m, i64 n, const typename El
     ew_2d<S, 2, false>(m, n, p, l, vec, [&](const S(&x)[2]) { return E::store(apply_map(FN, E::load(x[1]))); });
 }
 
+template <typename C>
+__device__ __forceinline__ C apply_combine(int fn, C a, C b) {
+    switch (fn) {
+    case ELX_COMBINE_ADD: return a + b;
+    case ELX_COMBINE_SUB: return b - a;
+    case ELX_COMBINE_MUL: return a * b;
+    case ELX_COMBINE_DIV: return b / a;
+    case ELX_COMBINE_MAX: return a > b ? a : b;
+    case ELX_COMBINE_MIN: return a < b ? a : b;
+    case ELX_COMBINE_RELU_GRAD: return a > C(0) ? b : C(0);
+    default: return b;
+    }
+}
+
+// B := f(A, B) (CombineImpl.hpp:47-213): operand 0 is B, read and written
+template <typename T, int FN>
+__global__ __launch_bounds__(NT) void combine_kernel(i64 m, i64 n, const typename Elem<T>::storage* A, i64 lda,
+                                                     typename Elem<T>::storage* B, i64 ldb, bool vec) {
+    using E = Elem<T>;
+    using S = typename E::storage;
+    S* const p[2] = {B, const_cast<S*>(A)};
+    const i64 l[2] = {ldb, lda};
+    ew_2d<S, 2, true>(m, n, p, l, vec,
+                      [&](const S(&x)[2]) { return E::store(apply_combine(FN, E::load(x[1]), E::load(x[0]))); });
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>::storage* A, i64 lda, i64 i0,
                                                   i64 istride, i64 j0, i64 jstride, uint64_t seed,
@@ -450,6 +476,27 @@ hipError_t entrywise_map(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda
         default: return hipErrorInvalidValue;
     });
 #undef ELX_MAP_CASE
+    return hipGetLastError();
+}
+
+template <typename T, int FN>
+static void launch_combine(hipStream_t s, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb) {
+    using S = typename Elem<T>::storage;
+    const EwShape g = ew_shape<S>(m, n, {{A, lda}, {B, ldb}});
+    hipLaunchKernelGGL((combine_kernel<T, FN>), g.grid, dim3(NT), 0, s, g.m, g.n, static_cast<const S*>(A), lda,
+                       static_cast<S*>(B), ldb, g.vec);
+}
+
+hipError_t combine(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+#define ELX_COMBINE_CASE(F) case F: launch_combine<T, F>(s, m, n, A, lda, B, ldb); break;
+    ELX_DTYPE_SWITCH(dtype, T, switch (fn) {
+        ELX_COMBINE_CASE(ELX_COMBINE_ADD) ELX_COMBINE_CASE(ELX_COMBINE_SUB) ELX_COMBINE_CASE(ELX_COMBINE_MUL)
+        ELX_COMBINE_CASE(ELX_COMBINE_DIV) ELX_COMBINE_CASE(ELX_COMBINE_MAX) ELX_COMBINE_CASE(ELX_COMBINE_MIN)
+        ELX_COMBINE_CASE(ELX_COMBINE_RELU_GRAD)
+        default: return hipErrorInvalidValue;
+    });
+#undef ELX_COMBINE_CASE
     return hipGetLastError();
 }
 

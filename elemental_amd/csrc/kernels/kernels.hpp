@@ -76,6 +76,7 @@ hipError_t hadamard2d(int dtype, i64 m, i64 n, const void* A, i64 lda, const voi
                       void* C, i64 ldc, hipStream_t s);
 hipError_t entrywise_map(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb,
                          hipStream_t s);
+hipError_t combine(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void* B, i64 ldb, hipStream_t s);
 hipError_t fill_hash(int dtype, i64 m, i64 n, void* A, i64 lda, i64 i0, i64 istride, i64 j0,
                      i64 jstride, uint64_t seed, double center, double radius, hipStream_t s);
 

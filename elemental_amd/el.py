@@ -21,7 +21,7 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
 
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
-    "EntrywiseMap", "AxpyContract", "Transpose", "SetBlocksize", "Blocksize", "SetComputePanel",
+    "EntrywiseMap", "Combine", "AxpyContract", "Transpose", "SetBlocksize", "Blocksize", "SetComputePanel",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -255,6 +255,11 @@ def Hadamard(A, B, C):
 
 def EntrywiseMap(fn: int, A, B):
     call("elx_dm_entrywise_map", fn, A.h, B.h)
+
+
+def Combine(fn: int, A, B):
+    """B := f(A, B) entrywise on matching local blocks (ELX_COMBINE_* functors)."""
+    call("elx_dm_combine", fn, A.h, B.h)
 
 
 def AxpyContract(alpha, A, B):

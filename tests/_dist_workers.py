@@ -236,6 +236,19 @@ def blas1_worker(rank: int, world: int, port: int, height: int, device: int, see
         el.EntrywiseMap(el.L.MAP_SQUARE if hasattr(el, "L") else 3, Xm, F)
         want = oracle.local_block(Xg * Xg, el.STAR, el.VR, r, c, g.vc_rank, 0, F.RowAlign())
         assert np.array_equal(F.get_local(), want), "EntrywiseMap"
+        # Combine on matching [MC,MR] blocks: Yc := relu'(Xm) * Yc, then Yc := Yc - Xm
+        Yc.set_local(oracle.local_block(Yg - 0.5, el.MC, el.MR, r, c, g.vc_rank))
+        el.Combine(el.L.COMBINE_RELU_GRAD, Yc, Xm)  # Xm := (Yc > 0) ? Xm : 0
+        want = oracle.local_block(np.where(Yg - 0.5 > 0, Xg, 0.0), el.MC, el.MR, r, c, g.vc_rank)
+        assert np.array_equal(Xm.get_local(), want), "Combine relu_grad"
+        el.Combine(el.L.COMBINE_SUB, Xm, Yc)  # Yc := Yc - Xm
+        want = oracle.local_block((Yg - 0.5) - np.where(Yg - 0.5 > 0, Xg, 0.0), el.MC, el.MR, r, c, g.vc_rank)
+        assert np.array_equal(Yc.get_local(), want), "Combine sub"
+        try:
+            el.Combine(el.L.COMBINE_ADD, F, Yc)  # [STAR,VR] vs [MC,MR]: must refuse
+            raise AssertionError("Combine across distributions must raise")
+        except el.L.LogicError:
+            pass
         finish()
     except Exception:
         traceback.print_exc()

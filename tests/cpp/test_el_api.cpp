@@ -103,6 +103,13 @@ int main() {
     H.Resize(m, k);
     El::Hadamard(A, A, H);
     EXPECT(Local(H) == Local(Y));
+    El::Combine(A, H, El::CombineFn::SUB);  // H := H - A = A.*A - A
+    {
+        auto h = Local(H);
+        bool cok = true;
+        for (size_t i = 0; i < a.size(); ++i) cok &= h[i] == a[i] * a[i] - a[i];
+        EXPECT(cok);
+    }
     El::Zero(H);
     for (double v : Local(H)) EXPECT(v == 0.0);
 

@@ -185,6 +185,22 @@ def test_blas1_kernels(t, npdt):
     L.call("elx_entrywise_map", t, L.MAP_ABS, m, n, dX.data_ptr(), m, dZ.data_ptr(), m, None)
     sync()
     assert np.array_equal(_as_f64(host(dZ, (m, n), hostdt), npdt), np.abs(Xf))
+    # combine: B := f(A, B) (CombineImpl.hpp), every functor, in the compute type
+    cdt = np.float64 if t == L.F64 else np.float32
+    a, b = Xf.astype(cdt), Yf.astype(cdt)
+    funcs = {L.COMBINE_ADD: a + b, L.COMBINE_SUB: b - a, L.COMBINE_MUL: a * b, L.COMBINE_DIV: b / a,
+             L.COMBINE_MAX: np.maximum(a, b), L.COMBINE_MIN: np.minimum(a, b),
+             L.COMBINE_RELU_GRAD: np.where(a > 0, b, 0).astype(cdt)}
+    for fn, ref in funcs.items():
+        dB = dev(Y)
+        torch.cuda.synchronize()
+        L.call("elx_combine", t, fn, m, n, dX.data_ptr(), m, dB.data_ptr(), m, None)
+        sync()
+        got, want = _as_f64(host(dB, (m, n), hostdt), npdt), _as_f64(_round(ref, npdt), npdt)
+        if fn == L.COMBINE_DIV:
+            assert np.allclose(got, want, rtol=4 * np.finfo(cdt).eps if npdt in (np.float64, np.float32) else 1e-2)
+        else:
+            assert np.array_equal(got, want), fn
 
 
 @pytest.mark.parametrize("t,npdt", DTYPES)
