@@ -26,8 +26,6 @@
 //  * XCD-aware bijective workgroup remap (as gemm_mfma.hip).
 #include <hip/hip_runtime.h>
 #include <cstdint>
-#include <cstdlib>
-#include <string>
 #include "kernels.hpp"
 #include "elem.hpp"
 
@@ -261,124 +259,9 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
     }
 }
 
-// ---------------------------------------------------------------------------
-// Deep-prefetch variant: BK = 32 K-tiles in a 4-slot LDS ring (128 KiB) with 3
-// tiles in flight.  Each K-tile is waited for with a COUNTED vmcnt (the tiles
-// behind it stay in flight) and a raw s_barrier (__syncthreads would drain
-// every DMA), then the tile DIST ahead is issued into the slot every wave
-// finished reading before that barrier.
-// ---------------------------------------------------------------------------
-namespace ring {
-constexpr int BK = 32, SLOTS = 4, DIST = 3;
-constexpr int HALF = 128 * BK * 2;  // 8 KiB
-constexpr int STAGE = 4 * HALF;     // 32 KiB: A halves 0,1 then B halves 0,1
-
-// KC rows are 64 B here (4 chunks): row r -> c ^ F((r>>2)&3), F = {0, 2, 3, 1};
-// makes the 16 lanes of each ds_read_b128 group distinct 16-B bank slots.
-__device__ __forceinline__ int swz_kc(int r) { return (((r >> 2) & 1) << 1) ^ (((r >> 3) & 1) * 3); }
-
-template <bool KC>
-__device__ __forceinline__ void stage_half(const uint16_t* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
-                                           int l) {
-    const int ins = w;  // 8 wave-instructions of 1 KiB, one per wave
-    if (KC) {           // 16 rows of 64 B per instruction
-        const int r = ins * 16 + (l >> 2);
-        const int c = (l & 3) ^ swz_kc(r);
-        i64 row = R + r;
-        row = row < rows ? row : rows - 1;
-        glds16(X + row * ld + k0 + 8 * c, img + ins * 1024);
-    } else {            // 4 k-rows of 256 B per instruction
-        const int kk = ins * 4 + (l >> 4);
-        const int c = (l & 15) ^ swz_rc(kk);
-        i64 col = R + 8 * c;
-        col = col <= rows - 8 ? col : rows - 8;
-        glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
-    }
-}
-
-template <bool KC>
-__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int l) {
-    if (KC) {
-        const int row = R0 + (l & 15), c = l >> 4;
-        return *(const __attribute__((address_space(3))) u32x4*)(img + row * 64 + ((c ^ swz_kc(row)) << 4));
-    }
-    return kern::frag<false>(img, R0, 0, l);  // 256-B k-rows: the BK = 64 RC image's layout
-}
-
 template <bool BF16, bool KCA, bool KCB>
-__device__ __forceinline__ void step(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
-                                     const lds_char* __restrict__ cur, f32x4 (&acc)[8][4]) {
-    if (more) {
-        stage_half<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_half<KCA>(f.A, f.lda, f.m, f.m0 + 128, knext, next + HALF, f.w, f.l);
-        stage_half<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + 2 * HALF, f.w, f.l);
-        stage_half<KCB>(f.B, f.ldb, f.n, f.n0 + 128, knext, next + 3 * HALF, f.w, f.l);
-    }
-    const lds_char* Ah = cur + f.wr * HALF;
-    const lds_char* Bh = cur + 2 * HALF + (f.wc >> 1) * HALF;
-    const int bc = (f.wc & 1) * 64;
-    u32x4 a[8], b[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) b[ni] = frag<KCB>(Bh, bc + ni * 16, f.l);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) a[mi] = frag<KCA>(Ah, mi * 16, f.l);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma<BF16>(a[mi], b[ni], acc[mi][ni]);
-}
-}  // namespace ring
-
-template <bool BF16, bool KCA, bool KCB>
-__global__ __launch_bounds__(NT, 1) void gemm_h256r_kernel(H2Params p) {
-    __shared__ __attribute__((aligned(1024))) char lds_raw[ring::SLOTS * ring::STAGE];
-    lds_char* lds = (lds_char*)lds_raw;
-    const int tid = threadIdx.x, l = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 2, wc = w & 3;
-    int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
-    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
-    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
-
-    const int nt = (int)(p.k / ring::BK);
-    auto stage = [&](int t, lds_char* st) {
-        const i64 k0 = (i64)t * ring::BK;
-        ring::stage_half<KCA>(f.A, f.lda, f.m, m0, k0, st, w, l);
-        ring::stage_half<KCA>(f.A, f.lda, f.m, m0 + 128, k0, st + ring::HALF, w, l);
-        ring::stage_half<KCB>(f.B, f.ldb, f.n, n0, k0, st + 2 * ring::HALF, w, l);
-        ring::stage_half<KCB>(f.B, f.ldb, f.n, n0 + 128, k0, st + 3 * ring::HALF, w, l);
-    };
-#pragma unroll
-    for (int d = 0; d < ring::DIST; ++d)
-        if (d < nt) stage(d, lds + d * ring::STAGE);
-    for (int t = 0; t < nt; ++t) {
-        // K-tile t has landed once at most the 4 DMAs of each later in-flight tile remain
-        const int ahead = min(ring::DIST - 1, nt - 1 - t);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave: tile t landed, tile t-1 read
-        const int tn_ = t + ring::DIST;
-        ring::step<BF16, KCA, KCB>(f, (i64)tn_ * ring::BK, tn_ < nt, lds + (tn_ % ring::SLOTS) * ring::STAGE,
-                                   lds + (t % ring::SLOTS) * ring::STAGE, acc);
-    }
-    epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
-}
-
-template <bool BF16, bool KCA, bool KCB>
-hipError_t launch_h256(const H2Params& p, hipStream_t s, bool use_ring) {
-    if (use_ring)
-        hipLaunchKernelGGL((gemm_h256r_kernel<BF16, KCA, KCB>), dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
-    else
-        hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
+hipError_t launch_h256(const H2Params& p, hipStream_t s) {
+    hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
     return hipGetLastError();
 }
 
@@ -389,14 +272,9 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
     const bool kca = ta, kcb = !tb;
-    // "ring" (default): BK = 32 tiles, 4-slot LDS ring, 3 in flight; "dbuf": BK = 64,
-    // two stages (ELX_H16_KERNEL overrides, A/B measurements)
-    static const bool use_ring = [] {
-        const char* v = getenv("ELX_H16_KERNEL");
-        return v ? std::string(v) != "dbuf" : true;
-    }();
-    const int bk = use_ring ? ring::BK : BK;
-    const i64 kmain = k / bk * bk;
+    // (a 4-slot BK = 32 ring with 3 K-tiles in flight measured 5-10 % slower:
+    //  profiles/r01_h16_ring_ab.log)
+    const i64 kmain = k / BK * BK;
     // the large-tile path: 16-B aligned rows/columns for glds, RC operands a
     // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
     const bool ok = kmain > 0 && al16(A) && al16(B) && lda % 8 == 0 && ldb % 8 == 0 &&
@@ -407,14 +285,14 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0};
     hipError_t e;
     if (is_bf16) {
-        if (kca) e = kcb ? launch_h256<true, true, true>(p, s, use_ring) : launch_h256<true, true, false>(p, s, use_ring);
-        else e = kcb ? launch_h256<true, false, true>(p, s, use_ring) : launch_h256<true, false, false>(p, s, use_ring);
+        if (kca) e = kcb ? launch_h256<true, true, true>(p, s) : launch_h256<true, true, false>(p, s);
+        else e = kcb ? launch_h256<true, false, true>(p, s) : launch_h256<true, false, false>(p, s);
     } else {
-        if (kca) e = kcb ? launch_h256<false, true, true>(p, s, use_ring) : launch_h256<false, true, false>(p, s, use_ring);
-        else e = kcb ? launch_h256<false, false, true>(p, s, use_ring) : launch_h256<false, false, false>(p, s, use_ring);
+        if (kca) e = kcb ? launch_h256<false, true, true>(p, s) : launch_h256<false, true, false>(p, s);
+        else e = kcb ? launch_h256<false, false, true>(p, s) : launch_h256<false, false, false>(p, s);
     }
     if (e != hipSuccess || kmain == k) return e;
-    // k tail (< bk): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
+    // k tail (< 64): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
     const uint16_t* At = ta ? A + kmain : A + kmain * lda;
     const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
     return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);
