@@ -93,6 +93,9 @@ _SIGS = {
     "elx_dm_copy": (_i, [_vp, _vp]),
     "elx_dm_transpose": (_i, [_vp, _vp]),
     "elx_dm_fill_hash": (_i, [_vp, c_uint64, _d, _d]),
+    "elx_initialize_random": (_i, [_i, _i]),
+    "elx_dm_uniform": (_i, [_vp, _i64, _i64, _d, _d]),
+    "elx_dm_make_uniform": (_i, [_vp, _d, _d]),
     "elx_dm_synchronize": (_i, [_vp]),
     "elx_dm_axpy": (_i, [_d, _vp, _vp]),
     "elx_dm_scale": (_i, [_d, _vp]),

@@ -6,6 +6,7 @@
 #include "core/distmatrix.hpp"
 #include "core/redist.hpp"
 #include "core/gemm.hpp"
+#include "core/random.hpp"
 #include "core/exec.hpp"
 #include <string>
 
@@ -261,6 +262,15 @@ int elx_dm_copy(elx_dm_t B, elx_dm_t A) { return Guard([&] { Copy(M(A), M(B)); }
 int elx_dm_transpose(elx_dm_t A, elx_dm_t B) { return Guard([&] { Transpose(M(A), M(B)); }); }
 int elx_dm_fill_hash(elx_dm_t A, uint64_t seed, double center, double radius) {
     return Guard([&] { M(A).FillHash(seed, center, radius); });
+}
+int elx_initialize_random(int deterministic, int world_rank) {
+    return Guard([&] { InitializeRandom(deterministic != 0, world_rank); });
+}
+int elx_dm_uniform(elx_dm_t A, int64_t height, int64_t width, double center, double radius) {
+    return Guard([&] { Uniform(M(A), height, width, center, radius); });
+}
+int elx_dm_make_uniform(elx_dm_t A, double center, double radius) {
+    return Guard([&] { MakeUniform(M(A), center, radius); });
 }
 int elx_dm_synchronize(elx_dm_t A) { return Guard([&] { M(A).Synchronize(); }); }
 

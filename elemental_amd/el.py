@@ -21,7 +21,8 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
 
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
-    "EntrywiseMap", "Combine", "AxpyContract", "Transpose", "SetBlocksize", "Blocksize", "SetComputePanel",
+    "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
+    "Blocksize", "SetComputePanel",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -255,6 +256,17 @@ def Hadamard(A, B, C):
 
 def EntrywiseMap(fn: int, A, B):
     call("elx_dm_entrywise_map", fn, A.h, B.h)
+
+
+def InitializeRandom(deterministic: bool = True, world_rank: int = 0):
+    """El::InitializeRandom: seed (21 << 16) | rank when deterministic (random.cpp:24-35)."""
+    call("elx_initialize_random", int(deterministic), world_rank)
+
+
+def Uniform(A, height: int, width: int, center: float = 0.0, radius: float = 1.0):
+    """El::Uniform: the reference's mt19937 draws on RedundantRank 0, broadcast."""
+    call("elx_dm_uniform", A.h, height, width, center, radius)
+    return A
 
 
 def Combine(fn: int, A, B):

@@ -269,6 +269,12 @@ template <typename T> void Hadamard(const AbstractDistMatrix<T>& A, const Abstra
 enum class EntrywiseFn { IDENTITY = ELX_MAP_IDENTITY, NEGATE = ELX_MAP_NEGATE, ABS = ELX_MAP_ABS, SQUARE = ELX_MAP_SQUARE,
                          SQRT = ELX_MAP_SQRT, EXP = ELX_MAP_EXP, LOG = ELX_MAP_LOG, RELU = ELX_MAP_RELU,
                          SIGMOID = ELX_MAP_SIGMOID, RECIPROCAL = ELX_MAP_RECIP, TANH = ELX_MAP_TANH };
+enum class CombineFn { ADD = ELX_COMBINE_ADD, SUB = ELX_COMBINE_SUB, MUL = ELX_COMBINE_MUL, DIV = ELX_COMBINE_DIV,
+                       MAX = ELX_COMBINE_MAX, MIN = ELX_COMBINE_MIN, RELU_GRAD = ELX_COMBINE_RELU_GRAD };
+// B := f(A, B) (EntrywiseMap.hpp:187-202; the device functor is one of CombineFn)
+template <typename T> void Combine(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, CombineFn f) {
+    detail::Check(elx_dm_combine(static_cast<int>(f), A.h(), B.h()));
+}
 template <typename T> void EntrywiseMap(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, EntrywiseFn f) {
     detail::Check(elx_dm_entrywise_map(static_cast<int>(f), A.h(), B.h()));
 }
@@ -276,6 +282,17 @@ template <typename T, typename S> void AxpyContract(S alpha, const AbstractDistM
     detail::Check(elx_dm_axpy_contract(static_cast<double>(alpha), A.h(), B.h()));
 }
 // grid-independent synthetic fill (stands in for Uniform(A, m, n, center, radius) in benchmarks)
+// El::InitializeRandom (random.cpp:24-35); Initialize() seeds deterministically
+inline void InitializeRandom(bool deterministic = true, int worldRank = 0) {
+    detail::Check(elx_initialize_random(deterministic ? 1 : 0, worldRank));
+}
+// El::Uniform / MakeUniform (Uniform.cpp:18-66): the reference's draws bit for bit
+template <typename T> void MakeUniform(AbstractDistMatrix<T>& A, T center = T(0), double radius = 1.0) {
+    detail::Check(elx_dm_make_uniform(A.h(), static_cast<double>(center), radius));
+}
+template <typename T> void Uniform(AbstractDistMatrix<T>& A, Int m, Int n, T center = T(0), double radius = 1.0) {
+    detail::Check(elx_dm_uniform(A.h(), m, n, static_cast<double>(center), radius));
+}
 template <typename T> void HashFill(AbstractDistMatrix<T>& A, std::uint64_t seed, double center, double radius) {
     detail::Check(elx_dm_fill_hash(A.h(), seed, center, radius));
 }
@@ -283,8 +300,8 @@ template <typename T> void HashFill(AbstractDistMatrix<T>& A, std::uint64_t seed
 // ---- environment ------------------------------------------------------------------
 inline void SetBlocksize(Int nb) { detail::Check(elx_set_blocksize(nb)); }
 inline Int Blocksize() { return elx_blocksize(); }
-inline void Initialize() {}
-inline void Initialize(int&, char**&) {}
+inline void Initialize() { InitializeRandom(true, 0); }
+inline void Initialize(int&, char**&) { InitializeRandom(true, 0); }
 inline void Finalize() {}
 
 }  // namespace El

@@ -76,6 +76,15 @@ extern "C" {
 #define ELX_MAP_SIGMOID  8
 #define ELX_MAP_RECIP    9
 #define ELX_MAP_TANH     10
+/* binary functors for elx_combine: B(i,j) := f(A(i,j), B(i,j))
+ * (El::Combine, include/El/blas_like/level1/EntrywiseMap.hpp:170-202) */
+#define ELX_COMBINE_ADD       0   /* a + b                 */
+#define ELX_COMBINE_SUB       1   /* b - a                 */
+#define ELX_COMBINE_MUL       2   /* a * b                 */
+#define ELX_COMBINE_DIV       3   /* b / a                 */
+#define ELX_COMBINE_MAX       4   /* max(a, b)             */
+#define ELX_COMBINE_MIN       5   /* min(a, b)             */
+#define ELX_COMBINE_RELU_GRAD 6   /* a > 0 ? b : 0         */
 
 /* ---- errors / runtime --------------------------------------------------- */
 /* replaces hydrogen::HIPError / H_CHECK_HIP (include/hydrogen/device/gpu/rocm/ROCmError.hpp) */
@@ -149,6 +158,9 @@ int elx_hadamard2d(int dtype, int64_t m, int64_t n,
                    void* C, int64_t ldc, void* stream);
 int elx_entrywise_map(int dtype, int fn, int64_t m, int64_t n,
                       const void* A, int64_t lda, void* B, int64_t ldb, void* stream);
+/* replaces CombineImpl (include/hydrogen/blas/gpu/CombineImpl.hpp:47-213) */
+int elx_combine(int dtype, int fn, int64_t m, int64_t n,
+                const void* A, int64_t lda, void* B, int64_t ldb, void* stream);
 /* grid-independent synthetic fill: A(i,j) = center + radius*u(seed,i0+i,j0+j), u in [-1,1) */
 int elx_fill_hash(int dtype, int64_t m, int64_t n, void* A, int64_t lda,
                   int64_t i0, int64_t istride, int64_t j0, int64_t jstride,
@@ -229,6 +241,13 @@ int elx_dm_copy(elx_dm_t B, elx_dm_t A);
 int elx_dm_transpose(elx_dm_t A, elx_dm_t B);
 /* synthetic grid-independent fill from global indices (see elx_fill_hash) */
 int elx_dm_fill_hash(elx_dm_t A, uint64_t seed, double center, double radius);
+/* El::InitializeRandom(deterministic) (src/core/random.cpp:24-35): seed the
+ * process-global mt19937 with (secs << 16) | worldRank, secs = 21 if deterministic */
+int elx_initialize_random(int deterministic, int world_rank);
+/* El::Uniform / MakeUniform (src/matrices/random/independent/Uniform.cpp:18-66):
+ * the reference's draws, bit for bit, for the same grid and call order */
+int elx_dm_uniform(elx_dm_t A, int64_t height, int64_t width, double center, double radius);
+int elx_dm_make_uniform(elx_dm_t A, double center, double radius);
 int elx_dm_synchronize(elx_dm_t A);
 
 /* ---- distributed BLAS-1 front doors (include/El/blas_like/level1/) ---- */
@@ -237,6 +256,7 @@ int elx_dm_scale(double alpha, elx_dm_t A);                   /* Scale.hpp:18-31
 int elx_dm_zero(elx_dm_t A);                                  /* Zero.hpp             */
 int elx_dm_hadamard(elx_dm_t A, elx_dm_t B, elx_dm_t C);      /* Hadamard.hpp:107-131 */
 int elx_dm_entrywise_map(int fn, elx_dm_t A, elx_dm_t B);     /* EntrywiseMap.hpp:90-137 */
+int elx_dm_combine(int fn, elx_dm_t A, elx_dm_t B);           /* EntrywiseMap.hpp:187-202, per local block */
 /* reduce-scatter family: B += alpha * contract(A)  (AxpyContract.hpp:483-544) */
 int elx_dm_axpy_contract(double alpha, elx_dm_t A, elx_dm_t B);
 

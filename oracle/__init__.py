@@ -166,6 +166,31 @@ def cpu_threads() -> int:
     return int(lib().orc_cpu_threads())
 
 
+def mt_uniform(seed: int, count: int, lo: float, hi: float, kind: str = "f64") -> np.ndarray:
+    """The reference's SampleUniform / SampleBall (include/El/core/random/impl.hpp:113-139,
+    230-231): libstdc++ std::uniform_real_distribution over std::mt19937, restated
+    with numpy's MT19937 (same init_genrand seeding, same 32-bit outputs) and
+    libstdc++'s generate_canonical (two draws for double, one for float; a
+    result of 1 becomes the largest value below 1).  kind: f64 | f32 | f16 | bf16
+    (f16 draws in float and rounds to half, as cpu_half_type does)."""
+    rs = np.random.RandomState(seed & 0xFFFFFFFF)
+    if kind == "f64":
+        u = rs.randint(0, 2 ** 32, size=2 * count, dtype=np.uint32).astype(np.float64)
+        r = (u[0::2] + u[1::2] * 4294967296.0) / 18446744073709551616.0
+        r = np.where(r >= 1.0, np.nextafter(1.0, 0.0), r)
+        return r * (hi - lo) + lo
+    u = rs.randint(0, 2 ** 32, size=count, dtype=np.uint32).astype(np.float32)
+    r = u / np.float32(4294967296.0)
+    r = np.where(r >= 1, np.nextafter(np.float32(1), np.float32(0)), r).astype(np.float32)
+    a, b = np.float32(lo), np.float32(hi)
+    x = (r * (b - a) + a).astype(np.float32)
+    if kind == "f16":
+        return x.astype(np.float16)
+    if kind == "bf16":
+        return f32_to_bf16_bits(x)
+    return x
+
+
 def gemm_half(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """The reference's CPU half path: the naive loops of
     src/core/imports/blas/Gemm.hpp:47-260 with every operation rounded to half

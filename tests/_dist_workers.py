@@ -197,6 +197,37 @@ def cannon_worker(rank: int, world: int, port: int, height: int, device: int, dt
         raise
 
 
+def uniform_worker(rank: int, world: int, port: int, height: int, device: int):
+    """El::Uniform on a multi-rank grid (Uniform.cpp:53-66): every rank seeds
+    (21 << 16) | rank; RedundantRank 0 of each redundant group draws its local
+    block in column-major order and broadcasts it to the group."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        m, n = 11, 9
+        for (U, V) in ((el.MC, el.MR), (el.STAR, el.STAR), (el.MC, el.STAR), (el.STAR, el.MR), (el.VC, el.STAR)):
+            el.InitializeRandom(True, rank)
+            A = el.DistMatrix(g, el.F64, U, V, device)
+            el.Uniform(A, m, n, 0.0, 1.0)
+            lh, lw = A.LocalHeight(), A.LocalWidth()
+            # the drawer: the rank of this group whose coordinate along the uncovered
+            # grid dimension(s) is 0 (RedundantRank 0)
+            covers = {el.MC: "c", el.MR: "r", el.VC: "cr", el.VR: "cr", el.STAR: ""}
+            cov = covers[U] + covers[V]
+            mc, mr = g.mc_rank, g.mr_rank
+            d_mc = mc if "c" in cov else 0
+            d_mr = mr if "r" in cov else 0
+            drawer = d_mc + r * d_mr  # VC rank == world rank (column-major grid)
+            want = oracle.mt_uniform((21 << 16) | drawer, lh * lw, -1.0, 1.0).reshape((lh, lw), order="F")
+            assert np.array_equal(A.get_local(), want), (el.DIST_NAMES[U], el.DIST_NAMES[V], rank)
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 def blas1_worker(rank: int, world: int, port: int, height: int, device: int, seed: int):
     import oracle
     el, comm = init(rank, world, port)

@@ -128,3 +128,25 @@ def test_attach_caller_storage():
         C.Resize(3, 3)
     with pytest.raises(L.LogicError):
         el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU).attach(m, n, 0, 0, Cpad.ctypes.data, m - 1)
+
+
+@pytest.mark.parametrize("dt,kind", [(el.F64, "f64"), (el.F32, "f32"), (el.F16, "f16"), (el.BF16, "bf16")])
+def test_uniform_reproduces_reference_draws(dt, kind):
+    """El::InitializeRandom + El::Uniform on a 1x1 grid: the reference's mt19937
+    draws in column-major order (oracle.mt_uniform), bit for bit."""
+    import oracle
+    g = el.Grid()
+    el.InitializeRandom(True, 0)
+    A = el.DistMatrix(g, dt, el.MC, el.MR, el.CPU)
+    el.Uniform(A, 13, 7, 0.5, 0.5)
+    want = oracle.mt_uniform((21 << 16) | 0, 13 * 7, 0.0, 1.0, kind).reshape((13, 7), order="F")
+    got = A.get_local()
+    assert np.array_equal(got.view(np.uint16) if kind in ("f16", "bf16") else got,
+                          want.view(np.uint16) if kind == "f16" else want)
+    # the generator advances: a second call continues the same stream
+    B = el.DistMatrix(g, dt, el.MC, el.MR, el.CPU)
+    el.Uniform(B, 3, 2, 0.5, 0.5)
+    nxt = oracle.mt_uniform((21 << 16) | 0, 13 * 7 + 6, 0.0, 1.0, kind)[13 * 7:].reshape((3, 2), order="F")
+    got = B.get_local()
+    assert np.array_equal(got.view(np.uint16) if kind in ("f16", "bf16") else got,
+                          nxt.view(np.uint16) if kind == "f16" else nxt)

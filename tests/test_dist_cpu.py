@@ -52,5 +52,11 @@ def test_gemm_cannon(world, height):
 
 
 @pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_uniform_reference_draws(world, height):
+    """El::Uniform = the reference's per-rank mt19937 draws + redundant broadcast."""
+    _spawn(W.uniform_worker, world, height, el.CPU)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
 def test_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.CPU, 5)

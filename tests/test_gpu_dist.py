@@ -49,6 +49,11 @@ def test_gpu_cannon(world, height):
     _spawn(W.cannon_worker, world, height, el.GPU, el.F64, [(45, 37, 62), (16, 12, 130)], 5)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (4, 2)])
+def test_gpu_uniform_reference_draws(world, height):
+    _spawn(W.uniform_worker, world, height, el.GPU)
+
+
 def test_gpu_summa_f32():
     _spawn(W.gemm_worker, 2, 1, el.GPU, el.F32, [(65, 33, 97)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 8, 9)
 

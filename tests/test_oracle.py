@@ -126,3 +126,23 @@ def test_bf16_rounding_known_answers():
     # 1+2^-8 is a tie -> even (1.0); 1+1.5*2^-8 rounds up to 1+2^-7
     assert list(oracle.bf16_bits_to_f32(b)[:4]) == [1.0, 1.0, 1.0078125, -2.0]
     assert np.isinf(oracle.bf16_bits_to_f32(b)[5])
+
+
+def test_mt_uniform_matches_libstdcxx(tmp_path):
+    """oracle.mt_uniform (the reference's Uniform draws) against std::mt19937 +
+    std::uniform_real_distribution compiled from the same libstdc++."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = tmp_path / "uniform_ref"
+    src = os.path.join(os.path.dirname(__file__), "cpp", "uniform_ref.cpp")
+    subprocess.check_call([gxx, "-O2", "-std=c++17", src, "-o", str(exe)])
+    for seed in ((21 << 16) | 0, (21 << 16) | 3):
+        for kind, lo, hi in (("f64", -0.1, 0.1), ("f32", 0.0, 1.0), ("f64", 2.0, 5.0)):
+            out = subprocess.run([str(exe), str(seed), "257", str(lo), str(hi), kind], capture_output=True,
+                                 text=True, check=True).stdout.split()
+            want = np.array([float(x) for x in out], dtype=np.float64 if kind == "f64" else np.float32)
+            got = oracle.mt_uniform(seed, 257, lo, hi, kind)  # (%.9g round-trips a float exactly)
+            assert np.array_equal(got, want), (seed, kind)
