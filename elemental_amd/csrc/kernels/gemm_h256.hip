@@ -26,6 +26,7 @@
 //  * XCD-aware bijective workgroup remap (as gemm_mfma.hip).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "kernels.hpp"
 #include "elem.hpp"
 
@@ -181,7 +182,9 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
                                          int l);
 
 // KCA: op(A) k-contiguous (TA); KCB: op(B) k-contiguous (!TB).
-template <bool BF16, bool KCA, bool KCB>
+// FL: timing ablations only (wrong results): 1 = no staging after the first
+// K-tile, 2 = no barrier, 8 = raw barrier without the DMA wait
+template <bool BF16, bool KCA, bool KCB, int FL = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_h256_kernel(H2Params p) {
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;  // generic -> LDS address space
@@ -209,10 +212,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_h256_kernel(H2Params p) {
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        step<BF16, KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        step<BF16, KCA, KCB>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE,
+                             lds + cur * STAGE, acc);
         // the staged K-tile has landed and every wave is done reading the other
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (FL & 8) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!(FL & 2)) __syncthreads();
+        }
     }
 
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
@@ -261,7 +270,15 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
 
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h256(const H2Params& p, hipStream_t s) {
-    hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
+    static const int fl = [] { const char* v = getenv("ELX_H16_FLAGS"); return v ? atoi(v) : 0; }();
+    const dim3 grid(p.tiles_m * p.tiles_n);
+    if constexpr (BF16 && !KCA && KCB) {
+        if (fl == 1) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 1>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 2) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 2>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 3) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 3>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
+        if (fl == 8) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 8>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
+    }
+    hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), grid, dim3(NT), 0, s, p);
     return hipGetLastError();
 }
 
