@@ -227,6 +227,166 @@ __global__ __launch_bounds__(NT, 1) void gemm_h256_kernel(H2Params p) {
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
+// ---------------------------------------------------------------------------
+// Phased variant: same tile, images and fragments, but each K-tile runs as four
+// phases of 16 MFMAs (one 64 x 32 quadrant of the wave's 128 x 64 block), and
+// the two wave groups (wr = 0, 1: the two waves sharing a SIMD) run one barrier
+// apart, so in every barrier interval one wave of each SIMD issues MFMAs while
+// its partner issues the next phase's fragment reads and one image of staging
+// (cdna_hip_programming.md §5, "The 256^2 8-phase template").
+//
+// The four LDS images of a stage are the quadrant halves, not the wave-group
+// halves: A image h holds rows {64h..64h+63} of both 128-row groups (image row
+// r -> tile row 128(r>>6) + 64h + (r&63)), B image h holds columns
+// {32h..32h+31} of each wave column (r -> 64(r>>5) + 32h + (r&31)), so the
+// quadrant order (0,0) (0,1) (1,1) (1,0) consumes A0+B0, B1, A1, - and the
+// next K-tile's images are staged in that same order, one per phase.
+//
+// Ordering (P = phase index, two barriers per phase, group 1 one barrier late):
+//  RAW: an image staged in phase P is read in phase P+3 (P+4 for A0); every
+//       wave waits for it in phase P+2 (s_waitcnt vmcnt(4): the two images
+//       staged after it may stay in flight) before that phase's first barrier.
+//  WAR: an image is restaged >= 4 phases after its last read, whose
+//       completion the MFMAs of that phase already forced.
+__device__ __forceinline__ i64 img_row(bool isB, int h, int r) {
+    return isB ? (i64)((r >> 5) * 64 + h * 32 + (r & 31)) : (i64)((r >> 6) * 128 + h * 64 + (r & 63));
+}
+
+// Stage quadrant image `which` (0: A0, 1: A1, 2: B0, 3: B1) of K-tile k0: two
+// 1-KiB wave-instructions per wave.
+template <bool KC>
+__device__ __forceinline__ void stage_q(const Frame& f, int which, i64 k0, lds_char* img) {
+    const bool isB = which >= 2;
+    const int h = which & 1;
+    const uint16_t* X = isB ? f.B : f.A;
+    const i64 ld = isB ? f.ldb : f.lda, rows = isB ? f.n : f.m, R0 = isB ? f.n0 : f.m0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int ins = f.w + 8 * j;
+        if (KC) {
+            const int r = ins * 8 + (f.l >> 3);
+            const int c = (f.l & 7) ^ swz_kc(r);
+            i64 row = R0 + img_row(isB, h, r);
+            row = row < rows ? row : rows - 1;
+            glds16(X + row * ld + k0 + 8 * c, img + ins * 1024);
+        } else {
+            const int kk = ins * 4 + (f.l >> 4);
+            const int c = (f.l & 15) ^ swz_rc(kk);
+            i64 col = R0 + img_row(isB, h, 8 * c);
+            col = col <= rows - 8 ? col : rows - 8;
+            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+        }
+    }
+}
+
+__device__ __forceinline__ void bar8() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool BF16, int FL = 0>
+__device__ __forceinline__ void cluster(f32x4 (&acc)[8][4], int mq, int nq, const u32x4 (&a)[8], const u32x4 (&b)[4]) {
+    if (!(FL & 4)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                acc[mq * 4 + mi][nq * 2 + ni] = mfma<BF16>(a[s * 4 + mi], b[s * 2 + ni], acc[mq * 4 + mi][nq * 2 + ni]);
+    if (!(FL & 4)) __builtin_amdgcn_s_setprio(0);
+}
+
+// One K-tile: four phases over `cur`, staging K-tile knext into `next`.
+template <bool BF16, bool KCA, bool KCB, int FL = 0>
+__device__ __forceinline__ void step8(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
+                                      const lds_char* __restrict__ cur, f32x4 (&acc)[8][4]) {
+    u32x4 a[8], b0[4], b1[4];
+    const int ar = f.wr * 64, bcol = f.wc * 32;
+    auto load_a = [&](const lds_char* img) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) a[s * 4 + mi] = frag<KCA>(img, ar + mi * 16, s, f.l);
+    };
+    auto load_b = [&](u32x4 (&b)[4], const lds_char* img) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b[s * 2 + ni] = frag<KCB>(img, bcol + ni * 16, s, f.l);
+    };
+    // phase 0: quadrant (0,0)
+    load_b(b0, cur + 2 * HALF);
+    load_a(cur);
+    if (more) {
+        if (!(FL & 1)) stage_q<KCA>(f, 0, knext, next);
+        if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar8();
+    cluster<BF16, FL>(acc, 0, 0, a, b0);
+    bar8();
+    // phase 1: quadrant (0,1)
+    load_b(b1, cur + 3 * HALF);
+    if (more && !(FL & 1)) stage_q<KCB>(f, 2, knext, next + 2 * HALF);
+    if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    bar8();
+    cluster<BF16, FL>(acc, 0, 1, a, b1);
+    bar8();
+    // phase 2: quadrant (1,1)
+    load_a(cur + HALF);
+    if (more && !(FL & 1)) stage_q<KCB>(f, 3, knext, next + 3 * HALF);
+    bar8();
+    cluster<BF16, FL>(acc, 1, 1, a, b1);
+    bar8();
+    // phase 3: quadrant (1,0)
+    if (more && !(FL & 1)) stage_q<KCA>(f, 1, knext, next + HALF);
+    if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    bar8();
+    cluster<BF16, FL>(acc, 1, 0, a, b0);
+    bar8();
+}
+
+// FL: timing ablations only (wrong results): 1 = no staging after the first
+// K-tile, 2 = no counted vmcnt waits, 4 = no s_setprio
+template <bool BF16, bool KCA, bool KCB, int FL = 0>
+__global__ __launch_bounds__(NT, 1) void gemm_h8p_kernel(H2Params p) {
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    stage_q<KCA>(f, 0, 0, lds);
+    stage_q<KCA>(f, 1, 0, lds + HALF);
+    stage_q<KCB>(f, 2, 0, lds + 2 * HALF);
+    stage_q<KCB>(f, 3, 0, lds + 3 * HALF);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar8();
+    if (wr == 1) bar8();  // group 1 runs one barrier behind group 0
+    for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        step8<BF16, KCA, KCB, FL>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+    }
+    if (wr == 0) bar8();  // matches group 1's last barrier
+
+    epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
+}
+
 // C = alpha acc + beta C.  C/D map of 16x16x32: col = lane&15, rows 4*(lane>>4) + r
 // (r = 0..3), i.e. four consecutive rows of one column = one 8-B access per tile.
 template <bool BF16>
@@ -268,18 +428,35 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
     }
 }
 
+template <typename K>
+hipError_t launch(K kernel, const H2Params& p, hipStream_t s) {
+    hipLaunchKernelGGL(kernel, dim3(p.tiles_m * p.tiles_n), dim3(NT), 0, s, p);
+    return hipGetLastError();
+}
+
+// Default: the phased kernel.  ELX_H16_KERNEL=s selects the two-stage kernel;
+// ELX_H16_FLAGS picks a timing ablation (profiles/r01_h16_ablation.log) of the
+// two-stage bf16 NN or phased bf16 TN kernel.
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h256(const H2Params& p, hipStream_t s) {
     static const int fl = [] { const char* v = getenv("ELX_H16_FLAGS"); return v ? atoi(v) : 0; }();
-    const dim3 grid(p.tiles_m * p.tiles_n);
-    if constexpr (BF16 && !KCA && KCB) {
-        if (fl == 1) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 1>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 2) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 2>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 3) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 3>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 8) { hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB, 8>), grid, dim3(NT), 0, s, p); return hipGetLastError(); }
+    static const bool two_stage = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 's'; }();
+    if (two_stage) {
+        if constexpr (BF16 && !KCA && KCB) {
+            if (fl == 1) return launch(gemm_h256_kernel<BF16, KCA, KCB, 1>, p, s);
+            if (fl == 2) return launch(gemm_h256_kernel<BF16, KCA, KCB, 2>, p, s);
+            if (fl == 3) return launch(gemm_h256_kernel<BF16, KCA, KCB, 3>, p, s);
+            if (fl == 8) return launch(gemm_h256_kernel<BF16, KCA, KCB, 8>, p, s);
+        }
+        return launch(gemm_h256_kernel<BF16, KCA, KCB>, p, s);
     }
-    hipLaunchKernelGGL((gemm_h256_kernel<BF16, KCA, KCB>), grid, dim3(NT), 0, s, p);
-    return hipGetLastError();
+    if constexpr (BF16 && KCA && KCB) {
+        if (fl == 1) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 1>, p, s);
+        if (fl == 2) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 2>, p, s);
+        if (fl == 3) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 3>, p, s);
+        if (fl == 4) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 4>, p, s);
+    }
+    return launch(gemm_h8p_kernel<BF16, KCA, KCB>, p, s);
 }
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }

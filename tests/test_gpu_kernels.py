@@ -89,10 +89,11 @@ def test_local_gemm_known_answer_exact(k):
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-@pytest.mark.parametrize("shape", [(131, 77, 95), (2000, 2056, 200)])
+@pytest.mark.parametrize("shape", [(131, 77, 95), (2000, 2056, 200), (2048, 2312, 520)])
 def test_local_gemm_16bit(kind, ta, tb, shape):
     """(131, 77, 95): the 128x128 kernel; (2000, 2056, 200): the 256x256
-    glds/transposed-read kernel with ragged edge tiles plus the k-tail pass."""
+    glds/transposed-read kernel with ragged edge tiles plus the k-tail pass;
+    (2048, 2312, 520): 8 K-tiles through its pipeline."""
     m, n, k = shape
     if kind == "f16":
         A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, 21, 0, 1, np.float16)
