@@ -43,6 +43,21 @@ Grid::Grid(std::shared_ptr<Comm> world, int height, int order) : world_(std::mov
     vr_comm_ = world_->Split(0, VRRank());
     ELX_REQUIRE(mc_comm_->Size() == r_ && mr_comm_->Size() == c_ && vc_comm_->Size() == p_,
                 "grid communicator split produced inconsistent sizes");
+    int a = r_, b = c_;
+    while (b) { const int t = a % b; a = b; b = t; }
+    gcd_ = a;
+    md_rank_.assign(p_, 0);
+    md_perp_.assign(p_, 0);
+    for (int diag = 0; diag < gcd_; ++diag) {
+        int row = 0, col = diag;
+        for (int k = 0; k < LCM(); ++k) {
+            const int vc = row + r_ * col;
+            md_perp_[vc] = diag;
+            md_rank_[vc] = k;
+            row = (row + 1) % r_;
+            col = (col + 1) % c_;
+        }
+    }
 }
 
 Device Grid::CommDevice() const {
@@ -57,9 +72,9 @@ int Grid::Stride(Dist d) const {
     case Dist::VR: return p_;
     case Dist::STAR:
     case Dist::CIRC: return 1;
-    case Dist::MD: break;
+    case Dist::MD: return LCM();
     }
-    throw UnsupportedError("MD distributions are outside the GEMM path (SURVEY §2 row 4)");
+    throw LogicError("unknown distribution");
 }
 
 int Grid::DistRankOf(Dist d, int vc) const {
@@ -70,9 +85,9 @@ int Grid::DistRankOf(Dist d, int vc) const {
     case Dist::VR: return VROf(vc);
     case Dist::STAR:
     case Dist::CIRC: return 0;
-    case Dist::MD: break;
+    case Dist::MD: return MDRankOf(vc);
     }
-    throw UnsupportedError("MD distributions are outside the GEMM path");
+    throw LogicError("unknown distribution");
 }
 
 Comm& Grid::DistComm(Dist d) const {
@@ -91,7 +106,7 @@ Comm& Grid::DistComm(Dist d) const {
 namespace {
 bool ValidPair(Dist u, Dist v) {
     if (u == Dist::CIRC || v == Dist::CIRC) return u == Dist::CIRC && v == Dist::CIRC;
-    if (u == Dist::MD || v == Dist::MD) return false;  // out of scope
+    if (u == Dist::MD || v == Dist::MD) return u == Dist::STAR || v == Dist::STAR;  // [MD,*], [*,MD]
     if (u == Dist::STAR || v == Dist::STAR) return true;
     return (u == Dist::MC && v == Dist::MR) || (u == Dist::MR && v == Dist::MC);
 }
@@ -103,12 +118,9 @@ Dist Collect(Dist u) { return u == Dist::CIRC ? Dist::CIRC : Dist::STAR; }
 
 DistMatrix::DistMatrix(std::shared_ptr<Grid> g, DType t, Dist colDist, Dist rowDist, Device dev, int root)
     : grid_(std::move(g)), dtype_(t), cdist_(colDist), rdist_(rowDist), dev_(dev), root_(root) {
-    if (!ValidPair(colDist, rowDist)) {
-        if (colDist == Dist::MD || rowDist == Dist::MD)
-            throw UnsupportedError("[MD,*]/[*,MD] distributions are outside the GEMM path (SURVEY §2 row 4)");
+    if (!ValidPair(colDist, rowDist))
         throw LogicError(Cat("invalid distribution [", DistName(colDist), ",", DistName(rowDist), "]"));
-    }
-    ELX_REQUIRE(root >= 0 && root < grid_->Size(), "bad root ", root);
+    ELX_REQUIRE(root >= 0 && root < CrossSize(), "Invalid root ", root);
     if (dev == Device::GPU) stream_ = Runtime::Get().ComputeStream();
     SetLocalSizes();
 }
@@ -116,13 +128,25 @@ DistMatrix::DistMatrix(std::shared_ptr<Grid> g, DType t, Dist colDist, Dist rowD
 int DistMatrix::ColStride() const { return G().Stride(cdist_); }
 int DistMatrix::RowStride() const { return G().Stride(rdist_); }
 
+// The ranks that can hold data: CIRC's root, the root diagonal for [MD,*] /
+// [*,MD] (CrossComm = MDPerp, MD_STAR.cpp:166-167), everyone otherwise.
+int DistMatrix::CrossSize() const {
+    if (cdist_ == Dist::CIRC) return G().Size();
+    if (cdist_ == Dist::MD || rdist_ == Dist::MD) return G().GCD();
+    return 1;
+}
+bool DistMatrix::CrossOf(int vc) const {
+    if (cdist_ == Dist::CIRC) return vc == root_;
+    if (cdist_ == Dist::MD || rdist_ == Dist::MD) return G().MDPerpOf(vc) == root_;
+    return true;
+}
 int DistMatrix::ColRankOf(int vc) const {
-    if (cdist_ == Dist::CIRC) return vc == root_ ? 0 : -1;
-    return G().DistRankOf(cdist_, vc);
+    if (!CrossOf(vc)) return -1;
+    return cdist_ == Dist::CIRC ? 0 : G().DistRankOf(cdist_, vc);
 }
 int DistMatrix::RowRankOf(int vc) const {
-    if (rdist_ == Dist::CIRC) return vc == root_ ? 0 : -1;
-    return G().DistRankOf(rdist_, vc);
+    if (!CrossOf(vc)) return -1;
+    return rdist_ == Dist::CIRC ? 0 : G().DistRankOf(rdist_, vc);
 }
 Int DistMatrix::LocalHeightOf(int vc) const {
     if (!ParticipatingOf(vc)) return 0;
@@ -177,7 +201,7 @@ void DistMatrix::Empty() {
 // caller storage as this rank's local block; alignments become constrained.
 void DistMatrix::Attach(Int height, Int width, int colAlign, int rowAlign, void* buffer, Int ldim, int root) {
     ELX_REQUIRE(height >= 0 && width >= 0, "negative dimensions");
-    ELX_REQUIRE(root >= 0 && root < G().Size(), "invalid root ", root);
+    ELX_REQUIRE(root >= 0 && root < CrossSize(), "Invalid root ", root);
     const int cs = ColStride(), rs = RowStride();
     ELX_REQUIRE(colAlign >= 0 && colAlign < cs, "invalid col alignment ", colAlign);
     ELX_REQUIRE(rowAlign >= 0 && rowAlign < rs, "invalid row alignment ", rowAlign);
@@ -277,7 +301,9 @@ std::shared_ptr<DistMatrix> DistMatrix::View(const DistMatrix& A, Int i0, Int i1
 }
 
 std::shared_ptr<DistMatrix> DistMatrix::Like(Dist cd, Dist rd) const {
-    auto B = std::make_shared<DistMatrix>(grid_, dtype_, cd, rd, dev_, root_);
+    // the root carries over only within the same distribution (a CIRC root or a
+    // diagonal index means nothing to another pair)
+    auto B = std::make_shared<DistMatrix>(grid_, dtype_, cd, rd, dev_, cd == cdist_ && rd == rdist_ ? root_ : 0);
     B->stream_ = stream_;
     return B;
 }

@@ -16,6 +16,7 @@
 #include "../runtime/runtime.hpp"
 #include "../comm/comm.hpp"
 #include <memory>
+#include <vector>
 
 namespace elx {
 
@@ -44,6 +45,15 @@ public:
     int MCOf(int vc) const { return vc % r_; }
     int MROf(int vc) const { return vc / r_; }
     int VROf(int vc) const { return MROf(vc) + c_ * MCOf(vc); }
+    // diagonals (Grid.cpp:105-107,157-185): gcd(r,c) diagonals of lcm(r,c)
+    // ranks each; rank (mc,mr) lies on diagonal mod(mr - mc, gcd) at the
+    // position reached walking (0, diag) -> (+1, +1) mod (r, c)
+    int GCD() const { return gcd_; }
+    int LCM() const { return p_ / gcd_; }
+    int MDRankOf(int vc) const { return md_rank_[vc]; }
+    int MDPerpOf(int vc) const { return md_perp_[vc]; }
+    int MDRank() const { return MDRankOf(VCRank()); }
+    int MDPerpRank() const { return MDPerpOf(VCRank()); }
 
     Comm& MC() const { return *mc_comm_; }
     Comm& MR() const { return *mr_comm_; }
@@ -61,7 +71,8 @@ public:
 
 private:
     std::shared_ptr<Comm> world_, mc_comm_, mr_comm_, vc_comm_, vr_comm_;
-    int r_ = 1, c_ = 1, p_ = 1, mc_ = 0, mr_ = 0, order_ = ELX_COLUMN_MAJOR;
+    int r_ = 1, c_ = 1, p_ = 1, mc_ = 0, mr_ = 0, order_ = ELX_COLUMN_MAJOR, gcd_ = 1;
+    std::vector<int> md_rank_, md_perp_;
 };
 
 class DistMatrix {
@@ -86,7 +97,9 @@ public:
     int RowStride() const;
     int ColRank() const { return ColRankOf(G().VCRank()); }
     int RowRank() const { return RowRankOf(G().VCRank()); }
-    int ColRankOf(int vc) const;   // -1 when that rank holds nothing (CIRC non-root)
+    int CrossSize() const;         // number of roots a matrix of this distribution can have
+    bool CrossOf(int vc) const;    // does rank vc lie in the root slice (CIRC root / root diagonal)?
+    int ColRankOf(int vc) const;   // -1 when that rank holds nothing (CIRC non-root, off-root diagonal)
     int RowRankOf(int vc) const;
     int ColShift() const { return (int)Shift(ColRank(), calign_, ColStride()); }
     int RowShift() const { return (int)Shift(RowRank(), ralign_, RowStride()); }

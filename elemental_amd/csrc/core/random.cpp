@@ -26,6 +26,8 @@ std::mt19937& Generator() {
 // grid that neither distribution covers (ElementalMatrix RedundantComm).
 Comm* RedundantComm(const DistMatrix& A) {
     const Grid& g = A.G();
+    // [MD,*], [*,MD], [CIRC,CIRC]: self (MD_STAR.cpp:170-171, CIRC_CIRC.cpp:54-55)
+    if (A.ColDist() == Dist::MD || A.RowDist() == Dist::MD || A.ColDist() == Dist::CIRC) return nullptr;
     auto covers_mc = [](Dist d) { return d == Dist::MC || d == Dist::VC || d == Dist::VR; };
     auto covers_mr = [](Dist d) { return d == Dist::MR || d == Dist::VC || d == Dist::VR; };
     const bool mc = covers_mc(A.ColDist()) || covers_mc(A.RowDist());

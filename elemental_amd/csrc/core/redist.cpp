@@ -55,8 +55,10 @@ DimXfer Intersect(Int n, int ss, int rs, int as, int sd, int rd, int ad) {
     return x;
 }
 
-bool FixesMC(Dist d) { return d == Dist::MC || d == Dist::VC || d == Dist::VR; }
-bool FixesMR(Dist d) { return d == Dist::MR || d == Dist::VC || d == Dist::VR; }
+// does the distribution pin a rank's grid row / column?  (an MD index names one
+// rank of the root diagonal, so it pins both)
+bool FixesMC(Dist d) { return d == Dist::MC || d == Dist::VC || d == Dist::VR || d == Dist::MD; }
+bool FixesMR(Dist d) { return d == Dist::MR || d == Dist::VC || d == Dist::VR || d == Dist::MD; }
 
 // Is source rank s the designated sender of A's data to receiver d?
 bool Designated(const DistMatrix& A, int s, int d) {
@@ -257,6 +259,8 @@ std::shared_ptr<DistMatrix> LocalTransposed(const DistMatrix& A) {
 bool SameLocalLayout(const DistMatrix& A, Dist cd, Dist rd, int calign, int ralign) {
     const Grid& g = A.G();
     if (A.ColDist() == Dist::CIRC || cd == Dist::CIRC) return false;
+    // root-dependent participation: never reinterpret in place
+    if (A.ColDist() == Dist::MD || A.RowDist() == Dist::MD || cd == Dist::MD || rd == Dist::MD) return false;
     if (g.Stride(cd) != A.ColStride() || g.Stride(rd) != A.RowStride()) return false;
     for (int q = 0; q < g.Size(); ++q) {
         if (Shift(g.DistRankOf(cd, q), calign, g.Stride(cd)) != Shift(A.ColRankOf(q), A.ColAlign(), A.ColStride()))

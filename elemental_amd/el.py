@@ -26,13 +26,24 @@ __all__ = [
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
-    "ROW_MAJOR", "COLUMN_MAJOR", "DIST_NAMES", "VALID_DISTS", "np_dtype",
+    "ROW_MAJOR", "COLUMN_MAJOR", "DIST_NAMES", "VALID_DISTS", "cross_size", "np_dtype",
 ]
 
 DIST_NAMES = {MC: "MC", MD: "MD", MR: "MR", VC: "VC", VR: "VR", STAR: "STAR", CIRC: "CIRC"}
-# every element-wise distribution on the GEMM path (MD pairs are out of scope)
+# the 14 element-wise distributions of the reference (ElementMatrix/*.cpp)
 VALID_DISTS = [(MC, MR), (MC, STAR), (MR, MC), (MR, STAR), (STAR, MC), (STAR, MR), (STAR, STAR),
-               (STAR, VC), (STAR, VR), (VC, STAR), (VR, STAR), (CIRC, CIRC)]
+               (STAR, VC), (STAR, VR), (VC, STAR), (VR, STAR), (CIRC, CIRC), (MD, STAR), (STAR, MD)]
+
+
+def cross_size(U: int, V: int, r: int, c: int) -> int:
+    """How many roots a [U,V] matrix can have: CIRC -> any rank, MD -> the gcd(r,c)
+    diagonals (CrossComm = MDPerp), otherwise 1 (AbstractDistMatrix::SetRoot)."""
+    from math import gcd
+    if U == CIRC:
+        return r * c
+    if MD in (U, V):
+        return gcd(r, c)
+    return 1
 
 
 def np_dtype(t: int):
@@ -222,8 +233,11 @@ class DistMatrix:
         return self
 
     def like(self, U=None, V=None, device=None) -> "DistMatrix":
-        return DistMatrix(self.grid, self.dtype, self.U if U is None else U, self.V if V is None else V,
-                          self.device if device is None else device, self.root)
+        U = self.U if U is None else U
+        V = self.V if V is None else V
+        same = (U, V) == (self.U, self.V)  # a root means nothing to another distribution
+        return DistMatrix(self.grid, self.dtype, U, V, self.device if device is None else device,
+                          self.root if same else 0)
 
 
 # ------------------------------------------------------------ front doors

@@ -57,17 +57,39 @@ void orc_grid_coords(int r, int c, int order, int rank, int* mc, int* mr, int* v
     *vr = *mr + c * *mc;
 }
 
+static int gcd_int(int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; }
+
+/* Grid.cpp:105-107,157-185: diagonal index mod(mr - mc, gcd) and the position
+ * along it, reached by walking (0, diag) -> (+1, +1) mod (r, c). */
+void orc_md_coords(int r, int c, int vc, int* diag, int* pos) {
+    const int mc = vc % r, mr = vc / r, g = gcd_int(r, c), lcm = r * c / g;
+    int row = 0, col, k;
+    *diag = ((mr - mc) % g + g) % g;
+    col = *diag;
+    *pos = 0;
+    for (k = 0; k < lcm; ++k) {
+        if (row == mc && col == mr) { *pos = k; return; }
+        row = (row + 1) % r;
+        col = (col + 1) % c;
+    }
+}
+
 int orc_dist_stride(int dist, int r, int c) {
     switch (dist) {
     case D_MC: return r;
     case D_MR: return c;
     case D_VC: case D_VR: return r * c;
+    case D_MD: return r * c / gcd_int(r, c);  /* MD_STAR.cpp:193: LCM */
     default: return 1;
     }
 }
 
+/* rank of vc in `dist`; for MD the root names the diagonal that holds the
+ * matrix (CrossComm = MDPerp, MD_STAR.cpp:166-167) and the other diagonals
+ * hold nothing */
 int orc_dist_rank(int dist, int r, int c, int vc, int root) {
     const int mc = vc % r, mr = vc / r;
+    int diag, pos;
     switch (dist) {
     case D_MC: return mc;
     case D_MR: return mr;
@@ -75,6 +97,7 @@ int orc_dist_rank(int dist, int r, int c, int vc, int root) {
     case D_VR: return mr + c * mc;
     case D_STAR: return 0;
     case D_CIRC: return vc == root ? 0 : -1;
+    case D_MD: orc_md_coords(r, c, vc, &diag, &pos); return diag == root ? pos : -1;
     default: return -1;
     }
 }

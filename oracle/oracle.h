@@ -20,6 +20,7 @@ int64_t orc_max_length(int64_t n, int64_t stride);
 int orc_default_height(int p);
 void orc_grid_coords(int r, int c, int order, int rank, int* mc, int* mr, int* vc, int* vr);
 /* stride of / rank in a distribution (El::Dist ordinals); -1 = holds nothing */
+void orc_md_coords(int r, int c, int vc, int* diag, int* pos);
 int orc_dist_stride(int dist, int r, int c);
 int orc_dist_rank(int dist, int r, int c, int vc, int root);
 /* local block of global column-major G (es-byte elements) on VC rank vc,

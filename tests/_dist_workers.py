@@ -60,14 +60,14 @@ def redist_worker(rank: int, world: int, port: int, height: int, device: int, dt
         for (U, V) in pairs:
             ca = rng.randrange(oracle.lib().orc_dist_stride(U, r, c))
             ra = rng.randrange(oracle.lib().orc_dist_stride(V, r, c))
-            A = el.DistMatrix(g, dtype, U, V, device, root=world - 1)
+            A = el.DistMatrix(g, dtype, U, V, device, root=el.cross_size(U, V, r, c) - 1)
             A.Align(ca, ra)
             A.Resize(m, n)
-            A.set_local(oracle.local_block(G, U, V, r, c, g.vc_rank, ca, ra, world - 1))
+            A.set_local(oracle.local_block(G, U, V, r, c, g.vc_rank, ca, ra, A.root))
             for (X, Y) in pairs:
                 xa = rng.randrange(oracle.lib().orc_dist_stride(X, r, c))
                 ya = rng.randrange(oracle.lib().orc_dist_stride(Y, r, c))
-                B = el.DistMatrix(g, dtype, X, Y, device, root=rng.randrange(world))
+                B = el.DistMatrix(g, dtype, X, Y, device, root=rng.randrange(el.cross_size(X, Y, r, c)))
                 B.Align(xa, ya)
                 B.assign(A)
                 want = oracle.local_block(G, X, Y, r, c, g.vc_rank, xa, ya, B.root)
@@ -207,14 +207,16 @@ def uniform_worker(rank: int, world: int, port: int, height: int, device: int):
         g = el.Grid(comm, height)
         r, c = g.height, g.width
         m, n = 11, 9
-        for (U, V) in ((el.MC, el.MR), (el.STAR, el.STAR), (el.MC, el.STAR), (el.STAR, el.MR), (el.VC, el.STAR)):
+        for (U, V) in ((el.MC, el.MR), (el.STAR, el.STAR), (el.MC, el.STAR), (el.STAR, el.MR), (el.VC, el.STAR),
+                       (el.MD, el.STAR), (el.STAR, el.MD), (el.CIRC, el.CIRC)):
             el.InitializeRandom(True, rank)
             A = el.DistMatrix(g, el.F64, U, V, device)
             el.Uniform(A, m, n, 0.0, 1.0)
             lh, lw = A.LocalHeight(), A.LocalWidth()
             # the drawer: the rank of this group whose coordinate along the uncovered
             # grid dimension(s) is 0 (RedundantRank 0)
-            covers = {el.MC: "c", el.MR: "r", el.VC: "cr", el.VR: "cr", el.STAR: ""}
+            # (MD and CIRC: RedundantComm is self, every holder draws its own block)
+            covers = {el.MC: "c", el.MR: "r", el.VC: "cr", el.VR: "cr", el.STAR: "", el.MD: "cr", el.CIRC: "cr"}
             cov = covers[U] + covers[V]
             mc, mr = g.mc_rank, g.mr_rank
             d_mc = mc if "c" in cov else 0

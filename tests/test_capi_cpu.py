@@ -53,8 +53,10 @@ def test_error_mapping_and_messages():
     C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=4, width=3)
     with pytest.raises(L.LogicError, match="onformal|dimension|match"):
         el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, B, 0.0, C)
-    with pytest.raises(L.LogicError):
-        L.call("elx_dm_create", L.ctypes.byref(L.ctypes.c_void_p()), g.h, el.F64, el.MD, el.STAR, el.CPU, 0)
+    with pytest.raises(L.LogicError, match="invalid distribution"):
+        L.call("elx_dm_create", L.ctypes.byref(L.ctypes.c_void_p()), g.h, el.F64, el.MD, el.MR, el.CPU, 0)
+    with pytest.raises(L.LogicError, match="Invalid root"):  # one diagonal on a 1x1 grid
+        L.call("elx_dm_create", L.ctypes.byref(L.ctypes.c_void_p()), g.h, el.F64, el.MD, el.STAR, el.CPU, 1)
     with pytest.raises(L.LogicError, match="Unsupported Gemm option"):  # Cannon is NN only (NT.hpp:526)
         el.Gemm(el.NORMAL, el.TRANSPOSE, 1.0, A, el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=3, width=3),
                 0.0, C, alg=el.GEMM_CANNON)

@@ -22,9 +22,10 @@ def _spawn(fn, world, *args):
     mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world,height", [(2, 1), (2, 2), (4, 2)])
+@pytest.mark.parametrize("world,height", [(2, 1), (2, 2), (4, 2), (8, 2)])
 def test_redistribution_all_pairs_bit_exact(world, height):
-    """tests/core/DistMatrix.cpp: every [X,Y] <- [U,V] with random alignments."""
+    """tests/core/DistMatrix.cpp: every [X,Y] <- [U,V] of the 14 distributions
+    with random alignments and roots (2x4: MD diagonals of length lcm = 4)."""
     _spawn(W.redist_worker, world, height, el.CPU, el.F64, 13, 11, 1234 + world + height)
 
 

@@ -12,7 +12,7 @@ import pytest
 import oracle
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-NAME = {"MC": oracle.MC, "MR": oracle.MR, "VC": oracle.VC, "VR": oracle.VR, "STAR": oracle.STAR,
+NAME = {"MC": oracle.MC, "MD": oracle.MD, "MR": oracle.MR, "VC": oracle.VC, "VR": oracle.VR, "STAR": oracle.STAR,
         "CIRC": oracle.CIRC}
 
 
@@ -35,7 +35,7 @@ def test_layout_matches_golden_every_rank():
         assert got.shape == want.shape, key
         assert np.array_equal(got, want), key
         checked += 1
-    assert checked == 336
+    assert checked == 392
 
 
 def test_layout_round_trip_place_block():

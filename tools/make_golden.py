@@ -15,7 +15,8 @@ code independent of oracle/oracle.c, so that they pin the oracle:
                Length = number of i in [0,n) with i = shift mod stride),
                grid ranks (src/core/Grid.cpp:58-206: column-major VC,
                mc = vc mod r, mr = vc div r, vr = mr + c*mc), [CIRC,CIRC]
-               only on root (ElementMatrix/CIRC_CIRC.cpp).
+               only on root (ElementMatrix/CIRC_CIRC.cpp), [MD,*]/[*,MD]
+               only on the root diagonal, stride lcm(r,c) (MD_STAR.cpp).
   hash.npz     hash_unit(seed,i,j) for seeds 1..3 (the synthetic Uniform
                input of SURVEY §8d; splitmix64 as published by Steele/Vigna).
   gemm_exact.npz  small integer-valued GEMMs in all four orientations with
@@ -37,15 +38,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tests", "golden")
 
 MC, MD, MR, VC, VR, STAR, CIRC = range(7)
-NAMES = {MC: "MC", MR: "MR", VC: "VC", VR: "VR", STAR: "STAR", CIRC: "CIRC"}
+NAMES = {MC: "MC", MD: "MD", MR: "MR", VC: "VC", VR: "VR", STAR: "STAR", CIRC: "CIRC"}
 PAIRS = [(MC, MR), (MC, STAR), (STAR, MR), (MR, MC), (MR, STAR), (STAR, MC), (VC, STAR), (STAR, VC),
-         (VR, STAR), (STAR, VR), (STAR, STAR), (CIRC, CIRC)]
+         (VR, STAR), (STAR, VR), (STAR, STAR), (CIRC, CIRC), (MD, STAR), (STAR, MD)]
 M64 = (1 << 64) - 1
+
+
+def diagonals(r: int, c: int) -> list[list[tuple[int, int]]]:
+    """Grid.cpp:105-107,157-185: gcd(r,c) diagonals; diagonal d lists the grid
+    coordinates (i mod r, (d + i) mod c), i = 0 .. lcm-1, in MD-rank order."""
+    from math import gcd
+    g = gcd(r, c)
+    lcm = r * c // g
+    return [[(i % r, (d + i) % c) for i in range(lcm)] for d in range(g)]
 
 
 def grid_ranks(vc: int, r: int, c: int) -> dict:
     mc, mr = vc % r, vc // r
-    return {MC: (mc, r), MR: (mr, c), VC: (vc, r * c), VR: (mr + c * mc, r * c), STAR: (0, 1), CIRC: (0, 1)}
+    diag = [(d, row.index((mc, mr))) for d, row in enumerate(diagonals(r, c)) if (mc, mr) in row][0]
+    return {MC: (mc, r), MR: (mr, c), VC: (vc, r * c), VR: (mr + c * mc, r * c), STAR: (0, 1), CIRC: (0, 1),
+            MD: (diag, len(diagonals(r, c)[0]))}
 
 
 def local_rows(n: int, rank: int, align: int, stride: int) -> list[int]:
@@ -57,6 +69,11 @@ def local_block(G: np.ndarray, U: int, V: int, r: int, c: int, vc: int, ca: int,
     if U == CIRC:
         return G.copy() if vc == root else np.zeros((0, 0), G.dtype)
     ranks = grid_ranks(vc, r, c)
+    if MD in (U, V):  # only the root diagonal holds the matrix (MD_STAR.cpp:166-167)
+        (diag, pos), lcm = ranks[MD]
+        if diag != root:
+            return np.zeros((0, 0), G.dtype)
+        ranks[MD] = (pos, lcm)
     cr, cs = ranks[U]
     rr, rs = ranks[V]
     rows = local_rows(G.shape[0], cr, ca, cs)
@@ -88,7 +105,7 @@ def make_layout() -> dict:
                 strides = grid_ranks(0, r, c)
                 ca = 0 if variant == 0 else (strides[U][1] - 1 if U != CIRC else 0)
                 ra = 0 if variant == 0 else (strides[V][1] // 2 if V != CIRC else 0)
-                root = 0 if variant == 0 else p - 1
+                root = 0 if variant == 0 else (len(diagonals(r, c)) - 1 if MD in (U, V) else p - 1)
                 for vc in range(p):
                     key = f"g{r}x{c}_{NAMES[U]}_{NAMES[V]}_a{ca}_{ra}_root{root}_vc{vc}"
                     out[key] = np.asfortranarray(local_block(G, U, V, r, c, vc, ca, ra, root))
