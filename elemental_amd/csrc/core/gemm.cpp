@@ -22,6 +22,7 @@
 //  * the _MS algorithm ids run the same pipelined variants (the reference's
 //    ROCm build rejects NT/TN _MS, TN.hpp:124-128).
 #include "gemm.hpp"
+#include <cstdlib>
 #include "redist.hpp"
 #include "exec.hpp"
 #include <algorithm>
@@ -34,6 +35,17 @@ Int g_blocksize = 128;      // src/core/environment.cpp:315
 Int g_compute_panel = 0;    // 0 = automatic
 int g_last_alg = ELX_GEMM_DEFAULT;
 constexpr Int kDotBlock = 2000;  // NN.hpp:578 (hard-coded in the reference)
+// On the GPU the Dot block is 2048, the reference's 2000 rounded up to the
+// 128-wide tile grid: a C block's elements are the same k-sums whatever the
+// m/n blocking, and 2000-wide blocks leave a ragged last tile per block and
+// 192-wide remainders (C4's 8192 = 4 x 2000 + 192).  C4 on one MI355X: 2000 ->
+// 124.4 TF, 2048 -> 131.1, 4096 -> 120.9, 8192 -> 121.4 (fewer, longer-k
+// launches over more tiles run slower: profiles/r01_dot_block.log).
+constexpr Int kDotBlockGPU = 2048;
+Int DotBlockGPU() {  // ELX_DOT_BLOCK overrides (tuning experiments)
+    static const Int v = [] { const char* e = getenv("ELX_DOT_BLOCK"); return e ? (Int)atoll(e) : kDotBlockGPU; }();
+    return v;
+}
 
 bool IsN(int o) { return o == ELX_NORMAL; }
 
@@ -525,7 +537,9 @@ void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B
     case ELX_GEMM_SUMMA_A_MS: case ELX_GEMM_SUMMA_A: SummaA(oA, oB, alpha, A, B, C); break;
     case ELX_GEMM_SUMMA_B_MS: case ELX_GEMM_SUMMA_B: SummaB(oA, oB, alpha, A, B, C); break;
     case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, beta, C); break;
-    case ELX_GEMM_SUMMA_DOT: SummaDot(oA, oB, alpha, A, B, C, kDotBlock); break;
+    case ELX_GEMM_SUMMA_DOT:
+        SummaDot(oA, oB, alpha, A, B, C, C.Dev() == Device::GPU ? DotBlockGPU() : kDotBlock);
+        break;
     case ELX_GEMM_CANNON:
         // Gemm.cpp:284-285: Cannon for NN; the other orientations' SUMMA switches
         // reject it (NT.hpp:526, TN.hpp:524, TT.hpp:435)

@@ -38,7 +38,7 @@ template <int BM_>
 struct Shape {
     static constexpr int BM = BM_, WM = BM_ / 32, NW = 2 * WM, NT = 64 * NW;
     static constexpr int IMGA = BM * BK * 8, IMGB = BN * BK * 8, STAGE = IMGA + IMGB;
-    static constexpr int MINB = BM == 128 ? 2 : 1;
+    static constexpr int WAVES_PER_EU = 4;  // 2 workgroups (BM 128) or 1 (BM 256) per CU: <= 128 VGPRs
 };
 
 struct GParams {
@@ -145,7 +145,7 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
 // timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7;
 // 8 = no wait for the DMA before the barrier, also wrong results)
 template <typename SH, bool KCA, bool KCB, bool BETA0, int FL = 0>
-__global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) {
+__global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GParams p) {
     constexpr int BM = SH::BM, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
@@ -193,6 +193,28 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f64g_kernel(GParams p) 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
     const int g = l >> 4, c = l & 15;
     const i64 ib = m0 + wr * 32, jb = n0 + wc * 64;
+    if (m0 + BM <= p.m && n0 + BN <= p.n) {
+        // interior tile: every C load issued before the first store (the guarded
+        // form below serializes load -> wait -> store per element)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {  // 16 loads in flight per half (VGPR budget: 4 waves per SIMD)
+            double cv[4][4];
+            if (!BETA0) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r];
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = p.alpha * acc[mi][ni][r];
+                    p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r] = BETA0 ? v : v + p.beta * cv[ni][r];
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
