@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3, "bf16": 2500.0, "f16": 2500.0}
 HBM_PEAK_GBS = 8000.0
 METRIC = "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak"
-KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_tile_kernel<float>",
+KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_f32g_kernel (LDS-DMA)",
           "bf16": "gemm_h8p_kernel<bf16>", "f16": "gemm_h8p_kernel<f16>"}
 
 
