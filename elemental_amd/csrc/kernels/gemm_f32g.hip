@@ -17,7 +17,9 @@
 //    k-rows a 32-lane half of a ds_read_b32 touches land in different 64-B halves.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "kernels.hpp"
+#include "lds_dma.hpp"
 
 namespace elx {
 namespace kern {
@@ -25,7 +27,6 @@ namespace kern {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 512, NW = 8, GROUP_M = 8;
 constexpr int IMG = 128 * BK * 4;  // 16 KiB per operand image
@@ -58,29 +59,24 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 __device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 5; }
 __device__ __forceinline__ int swz_rc(int kk) { return ((kk >> 3) & 1) << 2; }
 
-__device__ __forceinline__ void glds16(const float* src, lds_char* dst) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-}
-
 // 16 wave-instructions of 1 KiB per image; wave w issues w and w + 8.
-template <bool KC>
+template <bool BUF, bool KC>
 __device__ __forceinline__ void stage_img(const float* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
+    const DmaSrc<BUF, float> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? BM : BK) * ld * 4);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int ins = w + NW * q;
         if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
             const int r = ins * 8 + (l >> 3);
             const int c = (l & 7) ^ swz_kc(r);
-            i64 row = R + r;
-            row = row < rows ? row : rows - 1;
-            glds16(X + row * ld + k0 + 4 * c, img + ins * 1024);
+            const i64 row = R + r < rows ? r : rows - 1 - R;
+            src.load(row * ld + 4 * c, img + ins * 1024);
         } else {   // X(row, k) = X[row + k*ld]; 2 k-rows of 512 B per instruction
             const int kk = ins * 2 + (l >> 5);
             const int c = (l & 31) ^ swz_rc(kk);
-            i64 col = R + 4 * c;
-            col = col <= rows - 4 ? col : rows - 4;
-            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+            const i64 col = R + 4 * c <= rows - 4 ? 4 * c : rows - 4 - R;
+            src.load(col + kk * ld, img + ins * 1024);
         }
     }
 }
@@ -115,12 +111,12 @@ struct Frame {
 
 // __restrict__ LDS pointers: alias scopes so the in-flight DMA is not drained
 // before the ds_reads (see gemm_h256.hip).
-template <bool KCA, bool KCB>
+template <bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
                                      const lds_char* __restrict__ cur, f32x4 (&acc)[2][4]) {
     if (more) {
-        stage_img<KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+        stage_img<BUF, KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<BUF, KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
     }
     float a[2][8], b[4][8];
 #pragma unroll
@@ -136,7 +132,8 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi][s], b[ni][s], acc[mi][ni], 0, 0, 0);
 }
 
-template <bool KCA, bool KCB, bool BETA0>
+// BUF: staging through buffer descriptors (lds_dma.hpp) where the offsets fit.
+template <bool KCA, bool KCB, bool BETA0, bool BUF>
 __global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
@@ -162,13 +159,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    stage_img<BUF, KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<BUF, KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<KCA, KCB>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -194,12 +191,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
         }
 }
 
+template <bool KCA, bool KCB, bool BUF>
+hipError_t launch_fb(const FParams& p, hipStream_t s) {
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
+    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, true, BUF>), grid, dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, false, BUF>), grid, dim3(NT), 0, s, p);
+    return hipGetLastError();
+}
+
 template <bool KCA, bool KCB>
 hipError_t launch_f(const FParams& p, hipStream_t s) {
-    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, true>), grid, dim3(NT), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, false>), grid, dim3(NT), 0, s, p);
-    return hipGetLastError();
+    static const bool global_only = [] { const char* v = getenv("ELX_F32G_STAGE"); return v && v[0] == 'g'; }();
+    if (!global_only && dma_fits(KCA ? BM : BK, p.lda, 4) && dma_fits(KCB ? BN : BK, p.ldb, 4))
+        return launch_fb<KCA, KCB, true>(p, s);
+    return launch_fb<KCA, KCB, false>(p, s);
 }
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include "kernels.hpp"
+#include "lds_dma.hpp"
 
 namespace elx {
 namespace kern {
@@ -29,7 +30,6 @@ namespace kern {
 namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int BN = 128, BK = 16, GROUP_M = 8;
 // Tile shapes: BM = 128 (8 waves, 2 workgroups per CU) or 256 (16 waves, one
@@ -68,32 +68,27 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
     tn = inner / gsz;
 }
 
-__device__ __forceinline__ void glds16(const double* src, lds_char* dst) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-}
-
 // Stage one operand image (ROWS operand rows from global row R, 16 k from k0):
 // ROWS/8 wave-instructions of 1 KiB dealt over NW waves.
-template <bool KC, int ROWS, int NW>
+template <bool BUF, bool KC, int ROWS, int NW>
 __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
     constexpr int NINS = ROWS * BK * 8 / 1024;
+    const DmaSrc<BUF, double> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? ROWS : BK) * ld * 8);
 #pragma unroll
     for (int q = 0; q < NINS / NW; ++q) {
         const int ins = w + NW * q;
         if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
             const int r = ins * 8 + (l >> 3);
             const int c = (l & 7) ^ ((r >> 1) & 7);
-            i64 row = R + r;
-            row = row < rows ? row : rows - 1;
-            glds16(X + row * ld + k0 + 2 * c, img + ins * 1024);
+            const i64 row = R + r < rows ? r : rows - 1 - R;  // rows past the edge: any valid data
+            src.load(row * ld + 2 * c, img + ins * 1024);
         } else {   // X(row, k) = X[row + k*ld]; k-rows of ROWS*8 B, 1 KiB per instruction
             constexpr int IPR = ROWS * 8 / 1024;  // instructions per k-row
             const int kk = ins / IPR;
             const int c = ((ins % IPR) * 64 + l) ^ ((kk & 1) << 3);
-            i64 col = R + 2 * c;
-            col = col <= rows - 2 ? col : rows - 2;
-            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+            const i64 col = R + 2 * c <= rows - 2 ? 2 * c : rows - 2 - R;
+            src.load(col + kk * ld, img + ins * 1024);
         }
     }
 }
@@ -117,12 +112,12 @@ struct Frame {
 // One slab: stage slab t+1 into `next` and run slab t's MFMAs from `cur`.  The
 // __restrict__ LDS pointers give the inlined accesses alias scopes, so the
 // waitcnt pass does not drain the in-flight DMA before the ds_reads.
-template <typename SH, bool KCA, bool KCB>
+template <typename SH, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
                                      const lds_char* __restrict__ cur, f64x4 (&acc)[2][4]) {
     if (more) {
-        stage_img<KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<KCB, BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
+        stage_img<BUF, KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<BUF, KCB, BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
     }
     const lds_char* Ai = cur;
     const lds_char* Bi = cur + SH::IMGA;
@@ -143,8 +138,11 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
 
 // FL: diagnostic flags (1 = no staging after the first slab, 2 = no slab barrier:
 // timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7;
-// 8 = no wait for the DMA before the barrier, also wrong results)
-template <typename SH, bool KCA, bool KCB, bool BETA0, int FL = 0>
+// 8 = no wait for the DMA before the barrier, also wrong results).
+// BUF: stage through buffer descriptors (default where every lane offset of a
+// slab image fits the descriptor's 31-bit range): +2.5 % over global_load_lds
+// (profiles/r01_f64_buf.log).
+template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF, int FL = 0>
 __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GParams p) {
     constexpr int BM = SH::BM, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
@@ -171,8 +169,8 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
         for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
+    stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (FL & 4) {
@@ -180,7 +178,7 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     }
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<SH, KCA, KCB>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
         if (FL & 8) {  // raw barrier: no vmcnt drain (ablation only)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
@@ -233,20 +231,34 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
         }
 }
 
+template <typename K>
+hipError_t launch(K kernel, dim3 grid, int nt, const GParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(kernel, grid, dim3(nt), 0, s, p);
+    return hipGetLastError();
+}
+
+
+template <typename SH, bool KCA, bool KCB, bool BUF>
+hipError_t launch_b(const GParams& p, dim3 grid, hipStream_t s) {
+    static const int fl = [] { const char* v = getenv("ELX_F64G_FLAGS"); return v ? atoi(v) : 0; }();
+    if constexpr (!KCA && KCB) {  // timing ablations (NN, beta != 0 form)
+        if (fl == 1) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 1>, grid, SH::NT, p, s);
+        if (fl == 2) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 2>, grid, SH::NT, p, s);
+        if (fl == 4) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 4>, grid, SH::NT, p, s);
+        if (fl == 8) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 8>, grid, SH::NT, p, s);
+    }
+    if (p.beta == 0.0) return launch(gemm_f64g_kernel<SH, KCA, KCB, true, BUF>, grid, SH::NT, p, s);
+    return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF>, grid, SH::NT, p, s);
+}
+
 template <typename SH, bool KCA, bool KCB>
 hipError_t launch_g(GParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    static const int fl = [] { const char* v = getenv("ELX_F64G_FLAGS"); return v ? atoi(v) : 0; }();
-    if constexpr (!KCA && KCB) {
-        if (fl == 1) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 1>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 2) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 2>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 4) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 4>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
-        if (fl == 8) { hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false, 8>), grid, dim3(SH::NT), 0, s, p); return hipGetLastError(); }
-    }
-    if (p.beta == 0.0) hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, true>), grid, dim3(SH::NT), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f64g_kernel<SH, KCA, KCB, false>), grid, dim3(SH::NT), 0, s, p);
-    return hipGetLastError();
+    static const bool global_only = [] { const char* v = getenv("ELX_F64G_STAGE"); return v && v[0] == 'g'; }();
+    if (!global_only && dma_fits(KCA ? SH::BM : BK, p.lda, 8) && dma_fits(KCB ? BN : BK, p.ldb, 8))
+        return launch_b<SH, KCA, KCB, true>(p, grid, s);
+    return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
 
 template <typename SH>

@@ -28,6 +28,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include "kernels.hpp"
+#include "lds_dma.hpp"
 #include "elem.hpp"
 
 namespace elx {
@@ -41,7 +42,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512, GROUP_M = 8;
 constexpr int HALF = 128 * BK * 2;  // one half-tile image: 128 rows x 64 k x 2 B = 16 KiB
@@ -254,27 +254,29 @@ __device__ __forceinline__ i64 img_row(bool isB, int h, int r) {
 
 // Stage quadrant image `which` (0: A0, 1: A1, 2: B0, 3: B1) of K-tile k0: two
 // 1-KiB wave-instructions per wave.
-template <bool KC>
+template <bool BUF, bool KC>
 __device__ __forceinline__ void stage_q(const Frame& f, int which, i64 k0, lds_char* img) {
     const bool isB = which >= 2;
     const int h = which & 1;
     const uint16_t* X = isB ? f.B : f.A;
     const i64 ld = isB ? f.ldb : f.lda, rows = isB ? f.n : f.m, R0 = isB ? f.n0 : f.m0;
+    // offsets from the tile's corner at k0: < 256 operand rows (KC) or BK k-rows (RC) of ld
+    const DmaSrc<BUF, uint16_t> src(KC ? X + R0 * ld + k0 : X + R0 + k0 * ld, (KC ? 256 : BK) * ld * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int ins = f.w + 8 * j;
         if (KC) {
             const int r = ins * 8 + (f.l >> 3);
             const int c = (f.l & 7) ^ swz_kc(r);
-            i64 row = R0 + img_row(isB, h, r);
-            row = row < rows ? row : rows - 1;
-            glds16(X + row * ld + k0 + 8 * c, img + ins * 1024);
+            i64 row = img_row(isB, h, r);
+            row = R0 + row < rows ? row : rows - 1 - R0;
+            src.load(row * ld + 8 * c, img + ins * 1024);
         } else {
             const int kk = ins * 4 + (f.l >> 4);
             const int c = (f.l & 15) ^ swz_rc(kk);
-            i64 col = R0 + img_row(isB, h, 8 * c);
-            col = col <= rows - 8 ? col : rows - 8;
-            glds16(X + col + (k0 + kk) * ld, img + ins * 1024);
+            i64 col = img_row(isB, h, 8 * c);
+            col = R0 + col <= rows - 8 ? col : rows - 8 - R0;
+            src.load(col + kk * ld, img + ins * 1024);
         }
     }
 }
@@ -299,7 +301,7 @@ __device__ __forceinline__ void cluster(f32x4 (&acc)[8][4], int mq, int nq, cons
 }
 
 // One K-tile: four phases over `cur`, staging K-tile knext into `next`.
-template <bool BF16, bool KCA, bool KCB, int FL = 0>
+template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __device__ __forceinline__ void step8(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
                                       const lds_char* __restrict__ cur, f32x4 (&acc)[8][4]) {
     u32x4 a[8], b0[4], b1[4];
@@ -320,7 +322,7 @@ __device__ __forceinline__ void step8(const Frame& f, i64 knext, bool more, lds_
     load_b(b0, cur + 2 * HALF);
     load_a(cur);
     if (more) {
-        if (!(FL & 1)) stage_q<KCA>(f, 0, knext, next);
+        if (!(FL & 1)) stage_q<BUF, KCA>(f, 0, knext, next);
         if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -330,28 +332,29 @@ __device__ __forceinline__ void step8(const Frame& f, i64 knext, bool more, lds_
     bar8();
     // phase 1: quadrant (0,1)
     load_b(b1, cur + 3 * HALF);
-    if (more && !(FL & 1)) stage_q<KCB>(f, 2, knext, next + 2 * HALF);
+    if (more && !(FL & 1)) stage_q<BUF, KCB>(f, 2, knext, next + 2 * HALF);
     if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     bar8();
     cluster<BF16, FL>(acc, 0, 1, a, b1);
     bar8();
     // phase 2: quadrant (1,1)
     load_a(cur + HALF);
-    if (more && !(FL & 1)) stage_q<KCB>(f, 3, knext, next + 3 * HALF);
+    if (more && !(FL & 1)) stage_q<BUF, KCB>(f, 3, knext, next + 3 * HALF);
     bar8();
     cluster<BF16, FL>(acc, 1, 1, a, b1);
     bar8();
     // phase 3: quadrant (1,0)
-    if (more && !(FL & 1)) stage_q<KCA>(f, 1, knext, next + HALF);
+    if (more && !(FL & 1)) stage_q<BUF, KCA>(f, 1, knext, next + HALF);
     if (!(FL & 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     bar8();
     cluster<BF16, FL>(acc, 1, 0, a, b0);
     bar8();
 }
 
+// BUF: staging through buffer descriptors (lds_dma.hpp) where the offsets fit.
 // FL: timing ablations only (wrong results): 1 = no staging after the first
 // K-tile, 2 = no counted vmcnt waits, 4 = no s_setprio
-template <bool BF16, bool KCA, bool KCB, int FL = 0>
+template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_h8p_kernel(H2Params p) {
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
@@ -371,16 +374,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_h8p_kernel(H2Params p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_q<KCA>(f, 0, 0, lds);
-    stage_q<KCA>(f, 1, 0, lds + HALF);
-    stage_q<KCB>(f, 2, 0, lds + 2 * HALF);
-    stage_q<KCB>(f, 3, 0, lds + 3 * HALF);
+    stage_q<BUF, KCA>(f, 0, 0, lds);
+    stage_q<BUF, KCA>(f, 1, 0, lds + HALF);
+    stage_q<BUF, KCB>(f, 2, 0, lds + 2 * HALF);
+    stage_q<BUF, KCB>(f, 3, 0, lds + 3 * HALF);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar8();
     if (wr == 1) bar8();  // group 1 runs one barrier behind group 0
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        step8<BF16, KCA, KCB, FL>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        step8<BF16, KCA, KCB, BUF, FL>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
     }
     if (wr == 0) bar8();  // matches group 1's last barrier
 
@@ -434,6 +437,17 @@ hipError_t launch(K kernel, const H2Params& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+hipError_t launch_p(const H2Params& p, hipStream_t s, int fl) {
+    if constexpr (BF16 && KCA && KCB) {
+        if (fl == 1) return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF, 1>, p, s);
+        if (fl == 2) return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF, 2>, p, s);
+        if (fl == 3) return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF, 3>, p, s);
+        if (fl == 4) return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF, 4>, p, s);
+    }
+    return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF>, p, s);
+}
+
 // Default: the phased kernel.  ELX_H16_KERNEL=s selects the two-stage kernel;
 // ELX_H16_FLAGS picks a timing ablation (profiles/r01_h16_ablation.log) of the
 // two-stage bf16 NN or phased bf16 TN kernel.
@@ -450,13 +464,10 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
         }
         return launch(gemm_h256_kernel<BF16, KCA, KCB>, p, s);
     }
-    if constexpr (BF16 && KCA && KCB) {
-        if (fl == 1) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 1>, p, s);
-        if (fl == 2) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 2>, p, s);
-        if (fl == 3) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 3>, p, s);
-        if (fl == 4) return launch(gemm_h8p_kernel<BF16, KCA, KCB, 4>, p, s);
-    }
-    return launch(gemm_h8p_kernel<BF16, KCA, KCB>, p, s);
+    static const bool global_only = [] { const char* v = getenv("ELX_H16_STAGE"); return v && v[0] == 'g'; }();
+    if (!global_only && dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2))
+        return launch_p<BF16, KCA, KCB, true>(p, s, fl);
+    return launch_p<BF16, KCA, KCB, false>(p, s, fl);
 }
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
