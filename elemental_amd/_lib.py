@@ -97,6 +97,8 @@ _SIGS = {
     "elx_dm_uniform": (_i, [_vp, _i64, _i64, _d, _d]),
     "elx_dm_make_uniform": (_i, [_vp, _d, _d]),
     "elx_dm_synchronize": (_i, [_vp]),
+    "elx_dm_set_stream": (_i, [_vp, _vp]),
+    "elx_dm_stream": (_i, [_vp, POINTER(c_void_p)]),
     "elx_dm_axpy": (_i, [_d, _vp, _vp]),
     "elx_dm_scale": (_i, [_d, _vp]),
     "elx_dm_zero": (_i, [_vp]),

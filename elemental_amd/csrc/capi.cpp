@@ -273,6 +273,10 @@ int elx_dm_make_uniform(elx_dm_t A, double center, double radius) {
     return Guard([&] { MakeUniform(M(A), center, radius); });
 }
 int elx_dm_synchronize(elx_dm_t A) { return Guard([&] { M(A).Synchronize(); }); }
+int elx_dm_set_stream(elx_dm_t A, void* stream) {
+    return Guard([&] { M(A).SetSyncStream(stream ? static_cast<hipStream_t>(stream) : Runtime::Get().ComputeStream()); });
+}
+int elx_dm_stream(elx_dm_t A, void** stream) { return Guard([&] { *stream = M(A).Stream(); }); }
 
 int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y) { return Guard([&] { Axpy(alpha, M(X), M(Y)); }); }
 int elx_dm_scale(double alpha, elx_dm_t A) { return Guard([&] { Scale(alpha, M(A)); }); }

@@ -300,6 +300,17 @@ std::shared_ptr<DistMatrix> DistMatrix::View(const DistMatrix& A, Int i0, Int i1
     return V;
 }
 
+void DistMatrix::SetSyncStream(hipStream_t s) {
+    if (dev_ != Device::GPU || s == stream_) return;
+    hipEvent_t ev;
+    ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ELX_CHECK_HIP(hipEventRecord(ev, stream_));
+    ELX_CHECK_HIP(hipStreamWaitEvent(s, ev, 0));
+    ELX_CHECK_HIP(hipEventDestroy(ev));
+    stream_ = s;
+    if (buf_ && !viewing_) buf_->Rebind(s);
+}
+
 std::shared_ptr<DistMatrix> DistMatrix::Like(Dist cd, Dist rd) const {
     // the root carries over only within the same distribution (a CIRC root or a
     // diagonal index means nothing to another pair)

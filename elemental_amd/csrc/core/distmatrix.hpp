@@ -117,7 +117,10 @@ public:
     hipStream_t Stream() const { return stream_; }
     // Rebind the stream work on this matrix is ordered on.  Set it before the
     // first allocation: storage is returned to the pool on its allocation stream.
+    // internal: temporaries and views that live within one call
     void SetStream(hipStream_t s) { if (dev_ == Device::GPU) stream_ = s; }
+    // the public SetSyncInfo: ordered after the old stream, buffer rebound
+    void SetSyncStream(hipStream_t s);
     size_t ElemSize() const { return DTypeSize(dtype_); }
 
     // ---- realignment / resize (ElementMatrix.cpp:170-370 semantics) ----

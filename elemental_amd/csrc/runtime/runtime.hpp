@@ -62,6 +62,8 @@ public:
     // non-owning: caller storage (DistMatrix::Attach); never freed here
     void Wrap(Device d, void* ptr, size_t bytes) { Release(); dev_ = d; ptr_ = ptr; bytes_ = bytes; owned_ = false; }
     void Release();
+    // release on `s` from now on (the caller has ordered s after the old stream)
+    void Rebind(hipStream_t s) { stream_ = s; }
     void* data() const { return ptr_; }
     size_t bytes() const { return bytes_; }
     Device device() const { return dev_; }

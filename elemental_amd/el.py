@@ -210,6 +210,17 @@ class DistMatrix:
     def synchronize(self):
         call("elx_dm_synchronize", self.h)
 
+    def set_stream(self, stream: int | None):
+        """El::SetSyncInfo: queue this matrix's work on `stream` (a hipStream_t
+        handle, e.g. torch.cuda.Stream().cuda_stream; None = the library's)."""
+        call("elx_dm_set_stream", self.h, stream)
+
+    def stream(self) -> int | None:
+        """El::SyncInfoFromMatrix: the hipStream_t this matrix's work runs on."""
+        s = ctypes.c_void_p()
+        call("elx_dm_stream", self.h, ctypes.byref(s))
+        return s.value
+
     def __call__(self, rows, cols) -> "DistMatrix":
         """A(IR(i0,i1), IR(j0,j1)) view; rows/cols are (start, stop) or slice(None)."""
         i = self.info()

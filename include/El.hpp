@@ -172,6 +172,9 @@ public:
     void SetLocalBlock(const T* host, Int ld) { detail::Check(elx_dm_set_local(h(), host, ld)); }
     void GetLocalBlock(T* host, Int ld) const { detail::Check(elx_dm_get_local(h(), host, ld)); }
     void Synchronize() const { detail::Check(elx_dm_synchronize(h())); }
+    // SetSyncInfo(mat, si) / SyncInfoFromMatrix(mat): the matrix's HIP stream
+    void SetStream(void* stream) { detail::Check(elx_dm_set_stream(h(), stream)); }
+    void* Stream() const { void* s = nullptr; detail::Check(elx_dm_stream(h(), &s)); return s; }
     elx_dm_t h() const { return dm_.get(); }
 
 protected:

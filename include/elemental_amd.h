@@ -249,6 +249,12 @@ int elx_initialize_random(int deterministic, int world_rank);
 int elx_dm_uniform(elx_dm_t A, int64_t height, int64_t width, double center, double radius);
 int elx_dm_make_uniform(elx_dm_t A, double center, double radius);
 int elx_dm_synchronize(elx_dm_t A);
+/* El::SetSyncInfo / SyncInfoFromMatrix (include/El/core/Matrix/decl.hpp:523-535,
+ * impl_gpu.hpp:509-513): move the matrix's work to `stream` (ordered after the
+ * work already queued on its old stream; the local buffer is then released on
+ * the new one) / query it.  A no-op / NULL for CPU matrices. */
+int elx_dm_set_stream(elx_dm_t A, void* stream);
+int elx_dm_stream(elx_dm_t A, void** stream);
 
 /* ---- distributed BLAS-1 front doors (include/El/blas_like/level1/) ---- */
 int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y);       /* Axpy.hpp:151-176     */

@@ -149,3 +149,30 @@ def test_gpu_attach_torch_storage():
     want = oracle.gemm("N", "N", 1.0, Ah, Bh, 0.0, np.zeros((m, n), order="F"))
     assert oracle.parity_ratio(got[:m], want, Ah, Bh, k, np.finfo(np.float64).eps) <= 10
     assert (got[m:] == 3.0).all()
+
+
+def test_gpu_set_stream():
+    """El::SetSyncInfo / SyncInfoFromMatrix: a matrix moved to a caller stream
+    runs its work there, ordered after what was queued on its old stream."""
+    import torch
+    m, n, k = 257, 190, 300
+    g = el.Grid()
+    A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=m, width=k)
+    B = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=k, width=n)
+    C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=m, width=n)
+    A.fill_hash(1, 0.0, 1.0)
+    B.fill_hash(2, 0.0, 1.0)
+    C.fill_hash(3, 0.0, 1.0)
+    lib_stream = C.stream()
+    s = torch.cuda.Stream()
+    for M in (A, B, C):
+        M.set_stream(s.cuda_stream)
+        assert M.stream() == s.cuda_stream
+    el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
+    s.synchronize()
+    Ah, Bh, Ch = oracle.hash_matrix(m, k, 1), oracle.hash_matrix(k, n, 2), oracle.hash_matrix(m, n, 3)
+    want = oracle.gemm("N", "N", 0.5, Ah, Bh, -0.5, Ch)
+    assert oracle.parity_ratio(C.get_local(), want, Ah, Bh, k, np.finfo(np.float64).eps) <= 10
+    C.set_stream(None)  # back to the library's compute stream
+    assert C.stream() == lib_stream
+    el.device_synchronize()
