@@ -26,6 +26,7 @@ F32, F64, F16, BF16 = 0, 1, 2, 3
 (MAP_IDENTITY, MAP_NEGATE, MAP_ABS, MAP_SQUARE, MAP_SQRT, MAP_EXP, MAP_LOG, MAP_RELU, MAP_SIGMOID,
  MAP_RECIP, MAP_TANH) = range(11)
 (COMBINE_ADD, COMBINE_SUB, COMBINE_MUL, COMBINE_DIV, COMBINE_MAX, COMBINE_MIN, COMBINE_RELU_GRAD) = range(7)
+FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT = 0, 3, 4
 COLL_ALLGATHER, COLL_REDUCE_SCATTER, COLL_ALLTOALL, COLL_SENDRECV, COLL_BCAST, COLL_ALLREDUCE, \
     COLL_BARRIER = range(7)
 
@@ -99,6 +100,8 @@ _SIGS = {
     "elx_dm_synchronize": (_i, [_vp]),
     "elx_dm_set_stream": (_i, [_vp, _vp]),
     "elx_dm_stream": (_i, [_vp, POINTER(c_void_p)]),
+    "elx_dm_write": (_i, [_vp, c_char_p, _i, _i]),
+    "elx_dm_read": (_i, [_vp, c_char_p, _i, _i]),
     "elx_dm_axpy": (_i, [_d, _vp, _vp]),
     "elx_dm_scale": (_i, [_d, _vp]),
     "elx_dm_zero": (_i, [_vp]),

@@ -7,6 +7,7 @@
 #include "core/redist.hpp"
 #include "core/gemm.hpp"
 #include "core/random.hpp"
+#include "core/io.hpp"
 #include "core/exec.hpp"
 #include <string>
 
@@ -277,6 +278,18 @@ int elx_dm_set_stream(elx_dm_t A, void* stream) {
     return Guard([&] { M(A).SetSyncStream(stream ? static_cast<hipStream_t>(stream) : Runtime::Get().ComputeStream()); });
 }
 int elx_dm_stream(elx_dm_t A, void** stream) { return Guard([&] { *stream = M(A).Stream(); }); }
+int elx_dm_write(elx_dm_t A, const char* basename, int format, int int_bytes) {
+    return Guard([&] {
+        ELX_REQUIRE(basename != nullptr, "null file name");
+        Write(M(A), basename, format, int_bytes);
+    });
+}
+int elx_dm_read(elx_dm_t A, const char* filename, int format, int int_bytes) {
+    return Guard([&] {
+        ELX_REQUIRE(filename != nullptr, "null file name");
+        Read(M(A), filename, format, int_bytes);
+    });
+}
 
 int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y) { return Guard([&] { Axpy(alpha, M(X), M(Y)); }); }
 int elx_dm_scale(double alpha, elx_dm_t A) { return Guard([&] { Scale(alpha, M(A)); }); }

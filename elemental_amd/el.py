@@ -17,6 +17,7 @@ from . import _lib as L
 from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_CANNON, GEMM_DEFAULT,
                    GEMM_SUMMA_A, GEMM_SUMMA_A_MS, GEMM_SUMMA_B, GEMM_SUMMA_B_MS, GEMM_SUMMA_C,
                    GEMM_SUMMA_C_MS, GEMM_SUMMA_DOT, GPU, MC, MD, MR, NORMAL, ROW_MAJOR, STAR, TRANSPOSE,
+                   FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT,
                    VC, VR, call, lib)
 
 __all__ = [
@@ -26,7 +27,7 @@ __all__ = [
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
-    "ROW_MAJOR", "COLUMN_MAJOR", "DIST_NAMES", "VALID_DISTS", "cross_size", "np_dtype",
+    "ROW_MAJOR", "COLUMN_MAJOR", "FILE_AUTO", "FILE_BINARY", "FILE_BINARY_FLAT", "Write", "Read", "DIST_NAMES", "VALID_DISTS", "cross_size", "np_dtype",
 ]
 
 DIST_NAMES = {MC: "MC", MD: "MD", MR: "MR", VC: "VC", VR: "VR", STAR: "STAR", CIRC: "CIRC"}
@@ -291,6 +292,18 @@ def InitializeRandom(deterministic: bool = True, world_rank: int = 0):
 def Uniform(A, height: int, width: int, center: float = 0.0, radius: float = 1.0):
     """El::Uniform: the reference's mt19937 draws on RedundantRank 0, broadcast."""
     call("elx_dm_uniform", A.h, height, width, center, radius)
+    return A
+
+
+def Write(A, basename: str = "matrix", fmt: int = L.FILE_BINARY, int_bytes: int = 4):
+    """El::Write in the reference's BINARY (basename.bin: Int h, Int w, column-major
+    data) or BINARY_FLAT (basename.dat) format; int_bytes = sizeof(El::Int)."""
+    call("elx_dm_write", A.h, basename.encode(), fmt, int_bytes)
+
+
+def Read(A, filename: str, fmt: int = L.FILE_AUTO, int_bytes: int = 4):
+    """El::Read of a BINARY / BINARY_FLAT file into A's distribution and device."""
+    call("elx_dm_read", A.h, filename.encode(), fmt, int_bytes)
     return A
 
 

@@ -34,6 +34,8 @@ enum GemmAlgorithm {
     GEMM_SUMMA_C = ELX_GEMM_SUMMA_C, GEMM_SUMMA_DOT = ELX_GEMM_SUMMA_DOT, GEMM_CANNON = ELX_GEMM_CANNON
 };
 enum class Device : unsigned char { CPU = ELX_DEVICE_CPU, GPU = ELX_DEVICE_GPU };
+// include/El/core/types.hpp:543-559 (the formats of the GEMM path's fixtures)
+enum FileFormat { AUTO = ELX_FILE_AUTO, BINARY = ELX_FILE_BINARY, BINARY_FLAT = ELX_FILE_BINARY_FLAT };
 
 // 16-bit element types: gpu_half_type (rocblas_half in the reference,
 // include/hydrogen/utils/HalfPrecision.hpp:123) and bfloat16 (new).
@@ -298,6 +300,18 @@ template <typename T> void Uniform(AbstractDistMatrix<T>& A, Int m, Int n, T cen
 }
 template <typename T> void HashFill(AbstractDistMatrix<T>& A, std::uint64_t seed, double center, double radius) {
     detail::Check(elx_dm_fill_hash(A.h(), seed, center, radius));
+}
+
+// El::Write / El::Read (src/io/Write.cpp:70-86, src/io/Read.cpp:71-120); the file's
+// Int fields are sizeof(El::Int) of the producing build (4 by default)
+template <typename T>
+void Write(const AbstractDistMatrix<T>& A, const std::string& basename = "matrix", FileFormat format = BINARY,
+           int intBytes = 4) {
+    detail::Check(elx_dm_write(A.h(), basename.c_str(), static_cast<int>(format), intBytes));
+}
+template <typename T>
+void Read(AbstractDistMatrix<T>& A, const std::string& filename, FileFormat format = AUTO, int intBytes = 4) {
+    detail::Check(elx_dm_read(A.h(), filename.c_str(), static_cast<int>(format), intBytes));
 }
 
 // ---- environment ------------------------------------------------------------------

@@ -249,6 +249,18 @@ int elx_initialize_random(int deterministic, int world_rank);
 int elx_dm_uniform(elx_dm_t A, int64_t height, int64_t width, double center, double radius);
 int elx_dm_make_uniform(elx_dm_t A, double center, double radius);
 int elx_dm_synchronize(elx_dm_t A);
+/* El::Write / El::Read (src/io/Write.cpp:70-86, src/io/Read.cpp:71-120) in the
+ * reference's BINARY ([Int h][Int w][column-major data], file basename.bin)
+ * and BINARY_FLAT (data only, basename.dat; Read takes the size from A)
+ * formats; int_bytes = sizeof(El::Int) of the reference build (4 by default,
+ * 8 with Hydrogen_USE_64BIT_INTS); f16/bf16 travel as float like the
+ * reference's gpu_half_type overloads.  Read with ELX_FILE_AUTO detects the
+ * format from the extension. */
+#define ELX_FILE_AUTO        0
+#define ELX_FILE_BINARY      3
+#define ELX_FILE_BINARY_FLAT 4
+int elx_dm_write(elx_dm_t A, const char* basename, int format, int int_bytes);
+int elx_dm_read(elx_dm_t A, const char* filename, int format, int int_bytes);
 /* El::SetSyncInfo / SyncInfoFromMatrix (include/El/core/Matrix/decl.hpp:523-535,
  * impl_gpu.hpp:509-513): move the matrix's work to `stream` (ordered after the
  * work already queued on its old stream; the local buffer is then released on

@@ -286,3 +286,67 @@ def blas1_worker(rank: int, world: int, port: int, height: int, device: int, see
     except Exception:
         traceback.print_exc()
         raise
+
+
+def io_worker(rank: int, world: int, port: int, height: int, device: int, tmpdir: str):
+    """El::Write / El::Read in the reference's BINARY and BINARY_FLAT formats:
+    file bytes = [Int h][Int w][column-major data] (Write/Binary.hpp), read back
+    into other distributions bit-exactly (src/io/Read.cpp)."""
+    import oracle
+    import torch.distributed as dist
+    from elemental_amd import _lib as L
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        m, n = 13, 11
+        for dtype, npdt in ((el.F64, np.float64), (el.F32, np.float32), (el.F16, np.float16)):
+            G = oracle.hash_matrix(m, n, 17, 0.0, 3.0, npdt)
+            file_vals = G.astype(np.float32) if npdt == np.float16 else G  # half travels as float
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device)
+            A.Align(1 % r, 0)
+            A.Resize(m, n)
+            A.set_local(oracle.local_block(G, el.MC, el.MR, r, c, g.vc_rank, 1 % r, 0))
+            for int_bytes in (4, 8):
+                base = os.path.join(tmpdir, f"m{dtype}_{int_bytes}")
+                el.Write(A, base, el.FILE_BINARY, int_bytes)
+                dist.barrier()
+                raw = open(base + ".bin", "rb").read()
+                idt = np.int32 if int_bytes == 4 else np.int64
+                assert np.frombuffer(raw[:2 * int_bytes], dtype=idt).tolist() == [m, n]
+                body = np.frombuffer(raw[2 * int_bytes:], dtype=file_vals.dtype)
+                assert np.array_equal(body, np.asfortranarray(file_vals).ravel(order="F"))
+                for (U, V) in ((el.VC, el.STAR), (el.STAR, el.MR), (el.CIRC, el.CIRC), (el.MD, el.STAR)):
+                    B = el.DistMatrix(g, dtype, U, V, device)
+                    el.Read(B, base + ".bin", el.FILE_AUTO, int_bytes)
+                    i = B.info()
+                    assert (i["height"], i["width"]) == (m, n)
+                    want = oracle.local_block(G, U, V, r, c, g.vc_rank, i["col_align"], i["row_align"], 0)
+                    assert np.array_equal(B.get_local(), want), (dtype, el.DIST_NAMES[U], el.DIST_NAMES[V])
+                dist.barrier()
+            base = os.path.join(tmpdir, f"f{dtype}")
+            el.Write(A, base, el.FILE_BINARY_FLAT)
+            dist.barrier()
+            assert np.array_equal(np.fromfile(base + ".dat", dtype=file_vals.dtype),
+                                  np.asfortranarray(file_vals).ravel(order="F"))
+            C = el.DistMatrix(g, dtype, el.STAR, el.VR, device, height=m, width=n)
+            el.Read(C, base + ".dat")
+            i = C.info()
+            assert np.array_equal(C.get_local(), oracle.local_block(G, el.STAR, el.VR, r, c, g.vc_rank, 0,
+                                                                    i["row_align"], 0))
+            D = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m + 1, width=n)
+            try:
+                el.Read(D, base + ".dat")
+                raise AssertionError("a size mismatch must raise")
+            except L.ElxError as e:
+                assert "Expected file to be" in str(e)
+            dist.barrier()
+        try:
+            el.Read(A, os.path.join(tmpdir, "missing.bin"))
+            raise AssertionError("a missing file must raise")
+        except L.ElxError as e:
+            assert "Could not open" in str(e)
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise

@@ -3,6 +3,9 @@
 // El::Gemm code (tests/blas_like/Gemm.cpp:20-140 shape) and give the same
 // answers as a plain triple loop.  Built and run by tests/test_capi_cpu.py.
 #include <El.hpp>
+#include <unistd.h>
+#include <cstdio>
+#include <string>
 
 #include <cmath>
 #include <cstdio>
@@ -153,6 +156,16 @@ int main() {
         tok2 &= cbuf[m + j * (m + 2)] == 9.0 && cbuf[m + 1 + j * (m + 2)] == 9.0;
     }
     EXPECT(tok2);
+
+    // El::Write / El::Read round trip (BINARY: Int h, Int w, column-major data)
+    {
+        const std::string base = "/tmp/elx_api_test_" + std::to_string(::getpid());
+        El::Write(A, base, El::BINARY);
+        El::DistMatrix<double, El::VC, El::STAR> R(g);
+        El::Read(R, base + ".bin");
+        EXPECT(R.Height() == m && R.Width() == k && Local(R) == Local(A));
+        std::remove((base + ".bin").c_str());
+    }
 
     El::SetBlocksize(64);
     EXPECT(El::Blocksize() == 64);

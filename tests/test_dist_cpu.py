@@ -61,3 +61,9 @@ def test_uniform_reference_draws(world, height):
 @pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
 def test_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.CPU, 5)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_write_read_binary(world, height, tmp_path):
+    """El::Write / El::Read, BINARY and BINARY_FLAT (src/io/Write.cpp, Read.cpp)."""
+    _spawn(W.io_worker, world, height, el.CPU, str(tmp_path))

@@ -151,6 +151,11 @@ def test_gpu_attach_torch_storage():
     assert (got[m:] == 3.0).all()
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1)])
+def test_gpu_write_read_binary(world, height, tmp_path):
+    _spawn(W.io_worker, world, height, el.GPU, str(tmp_path))
+
+
 def test_gpu_set_stream():
     """El::SetSyncInfo / SyncInfoFromMatrix: a matrix moved to a caller stream
     runs its work there, ordered after what was queued on its old stream."""
