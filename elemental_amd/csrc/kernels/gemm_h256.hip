@@ -54,16 +54,17 @@ struct H2Params {
     const uint16_t* B; i64 ldb;
     uint16_t* C; i64 ldc;
     int tiles_m, tiles_n;
-    int vec_c;  // C base 8-B aligned and ldc % 4 == 0
+    int vec_c;    // C base 8-B aligned and ldc % 4 == 0
+    int group_m;  // tile-order group height (ELX_H16_GROUP, default GROUP_M)
 };
 
-__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int per_group = GROUP_M * tiles_n;
+    const int per_group = group_m * tiles_n;
     const int group = wg / per_group;
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int first_m = group * group_m;
+    const int gsz = min(tiles_m - first_m, group_m);
     const int inner = wg - group * per_group;
     tm = first_m + inner % gsz;
     tn = inner / gsz;
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_h256_kernel(H2Params p) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
     int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_h8p_kernel(H2Params p) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
     int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
@@ -472,6 +473,11 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
+int GroupM() {
+    static const int g = [] { const char* v = getenv("ELX_H16_GROUP"); return v ? atoi(v) : GROUP_M; }();
+    return g;
+}
+
 }  // namespace
 
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
@@ -487,7 +493,7 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                     ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 64 && m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0};
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM()};
     hipError_t e;
     if (is_bf16) {
         if (kca) e = kcb ? launch_h256<true, true, true>(p, s) : launch_h256<true, true, false>(p, s);
