@@ -10,9 +10,11 @@
 // round trip, no ds_write issue, no selects, and the next slab is in flight
 // across the MFMAs of the current one.
 //
-// Geometry: 128 x 128 tile, BK = 16, 8 waves of 32 x 64 (2 x 4 accumulators of
-// v_mfma_f64_16x16x4_f64), two LDS stages of 32 KiB -> two workgroups per CU
-// (4 waves per SIMD).  LDS images, 16-B chunk XOR swizzles applied to the
+// Geometry: 128 x 128 tile, BK = 16, two LDS stages of 32 KiB -> two workgroups
+// per CU.  Waves: 4 of 64 x 64 (4 x 4 accumulators of v_mfma_f64_16x16x4_f64,
+// 0.5 ds_read per MFMA, 2 waves per SIMD) for NN/TN/TT; 8 of 32 x 64 (2 x 4
+// accumulators, 4 waves per SIMD) for NT, where it measured faster
+// (profiles/r01_f64_wave.log).  LDS images, 16-B chunk XOR swizzles applied to the
 // glds SOURCE addresses (the DMA writes lane-linearly), conflict-free reads:
 //   KC (k contiguous in HBM): [128 rows][16 k] (128-B rows), chunk c -> c ^ ((r>>1)&7)
 //   RC (rows contiguous):     [16 k][128 rows] (1-KiB k-rows), chunk c -> c ^ 8(kk&1)
@@ -32,13 +34,15 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BN = 128, BK = 16, GROUP_M = 8;
-// Tile shapes: BM = 128 (8 waves, 2 workgroups per CU) or 256 (16 waves, one
-// workgroup per CU, 25 % fewer staged bytes per FLOP); waves are 32 x 64 each.
-template <int BM_>
+// Tile shapes: BM = 128 (two workgroups per CU) or 256 (one workgroup per CU,
+// 25 % fewer staged bytes per FLOP); wave tiles WTM x 64 with WTM = 32 (2 x 4
+// accumulators, 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read
+// per MFMA, half the waves).
+template <int BM_, int WTM_ = 32>
 struct Shape {
-    static constexpr int BM = BM_, WM = BM_ / 32, NW = 2 * WM, NT = 64 * NW;
+    static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW;
     static constexpr int IMGA = BM * BK * 8, IMGB = BN * BK * 8, STAGE = IMGA + IMGB;
-    static constexpr int WAVES_PER_EU = 4;  // 2 workgroups (BM 128) or 1 (BM 256) per CU: <= 128 VGPRs
+    static constexpr int WAVES_PER_EU = NW * (BM_ == 128 ? 2 : 1) / 4;  // waves resident per SIMD
 };
 
 struct GParams {
@@ -114,7 +118,7 @@ struct Frame {
 // waitcnt pass does not drain the in-flight DMA before the ds_reads.
 template <typename SH, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
-                                     const lds_char* __restrict__ cur, f64x4 (&acc)[2][4]) {
+                                     const lds_char* __restrict__ cur, f64x4 (&acc)[SH::MI][4]) {
     if (more) {
         stage_img<BUF, KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
         stage_img<BUF, KCB, BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
@@ -123,13 +127,13 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
     const lds_char* Bi = cur + SH::IMGA;
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
-        double a[2], b[4];
+        double a[SH::MI], b[4];
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) a[mi] = opnd<KCA, SH::BM>(Ai, f.wr * 32 + mi * 16, s, f.l);
+        for (int mi = 0; mi < SH::MI; ++mi) a[mi] = opnd<KCA, SH::BM>(Ai, f.wr * SH::WTM + mi * 16, s, f.l);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB, BN>(Bi, f.wc * 64 + ni * 16, s, f.l);
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;  // WM (M) x 2 (N) waves of 32 x 64
+    const int wr = w >> 1, wc = w & 1;  // WM (M) x 2 (N) waves of WTM x 64
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
@@ -162,9 +166,9 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     }
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
-    f64x4 acc[2][4];
+    f64x4 acc[SH::MI][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < SH::MI; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
@@ -190,12 +194,12 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
     const int g = l >> 4, c = l & 15;
-    const i64 ib = m0 + wr * 32, jb = n0 + wc * 64;
+    const i64 ib = m0 + wr * SH::WTM, jb = n0 + wc * 64;
     if (m0 + BM <= p.m && n0 + BN <= p.n) {
         // interior tile: every C load issued before the first store (the guarded
         // form below serializes load -> wait -> store per element)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {  // 16 loads in flight per half (VGPR budget: 4 waves per SIMD)
+        for (int mi = 0; mi < SH::MI; ++mi) {  // 16 loads in flight per 16-row block (VGPR budget: 4 waves per SIMD)
             double cv[4][4];
             if (!BETA0) {
 #pragma unroll
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
         return;
     }
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
             const i64 j = jb + ni * 16 + c;
@@ -287,7 +291,12 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
     GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), kchunk, m * n, gm, rm};
     static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();
-    if (bm == 256) return launch_shape<Shape<256>>(ta, !tb, p, s);
+    // wave tile: 64 x 64 (four waves) measured +1.5-2 % for NN/TN/TT; NT (both
+    // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
+    static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();
+    const int wtm = wtm_env ? wtm_env : (!ta && tb) ? 32 : 64;
+    if (bm == 256) return wtm == 64 ? launch_shape<Shape<256, 64>>(ta, !tb, p, s) : launch_shape<Shape<256>>(ta, !tb, p, s);
+    if (wtm == 64) return launch_shape<Shape<128, 64>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);
 }
 
