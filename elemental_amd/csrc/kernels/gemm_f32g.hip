@@ -28,7 +28,12 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 512, NW = 8, GROUP_M = 8;
+constexpr int BM = 128, BN = 128, BK = 32, GROUP_M = 8;
+// wave tile WTM x 64: WTM = 32 -> 8 waves (2 x 4 accumulators), 64 -> 4 waves (4 x 4)
+template <int WTM>
+struct WaveShape {
+    static constexpr int MI = WTM / 16, NW = 2 * BM / WTM, NT = 64 * NW;
+};
 constexpr int IMG = 128 * BK * 4;  // 16 KiB per operand image
 constexpr int STAGE = 2 * IMG;
 
@@ -59,13 +64,13 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 __device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 5; }
 __device__ __forceinline__ int swz_rc(int kk) { return ((kk >> 3) & 1) << 2; }
 
-// 16 wave-instructions of 1 KiB per image; wave w issues w and w + 8.
-template <bool BUF, bool KC>
+// 16 wave-instructions of 1 KiB per image; wave w issues w, w + NW, ...
+template <bool BUF, bool KC, int NW>
 __device__ __forceinline__ void stage_img(const float* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
     const DmaSrc<BUF, float> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? BM : BK) * ld * 4);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < 16 / NW; ++q) {
         const int ins = w + NW * q;
         if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
             const int r = ins * 8 + (l >> 3);
@@ -111,35 +116,37 @@ struct Frame {
 
 // __restrict__ LDS pointers: alias scopes so the in-flight DMA is not drained
 // before the ds_reads (see gemm_h256.hip).
-template <bool KCA, bool KCB, bool BUF>
+template <int WTM, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
-                                     const lds_char* __restrict__ cur, f32x4 (&acc)[2][4]) {
+                                     const lds_char* __restrict__ cur, f32x4 (&acc)[WTM / 16][4]) {
+    using WS = WaveShape<WTM>;
     if (more) {
-        stage_img<BUF, KCA>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<BUF, KCB>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+        stage_img<BUF, KCA, WS::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<BUF, KCB, WS::NW>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
     }
-    float a[2][8], b[4][8];
+    float a[WS::MI][8], b[4][8];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) frag<KCA>(cur, f.wr * 32 + mi * 16, f.l, a[mi]);
+    for (int mi = 0; mi < WS::MI; ++mi) frag<KCA>(cur, f.wr * WTM + mi * 16, f.l, a[mi]);
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) frag<KCB>(cur + IMG, f.wc * 64 + ni * 16, f.l, b[ni]);
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < WS::MI; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi][s], b[ni][s], acc[mi][ni], 0, 0, 0);
 }
 
 // BUF: staging through buffer descriptors (lds_dma.hpp) where the offsets fit.
-template <bool KCA, bool KCB, bool BETA0, bool BUF>
-__global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
+template <int WTM, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParams p) {
+    using WS = WaveShape<WTM>;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;  // 4 (M) x 2 (N) waves of 32 x 64
+    const int wr = w >> 1, wc = w & 1;  // BM/WTM (M) x 2 (N) waves of WTM x 64
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
@@ -152,29 +159,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
     }
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
-    f32x4 acc[2][4];
+    f32x4 acc[WS::MI][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WS::MI; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<BUF, KCA>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<BUF, KCB>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    stage_img<BUF, KCA, WS::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<BUF, KCB, WS::NW>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<WTM, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 
     // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
     const int g = l >> 4, c = l & 15;
-    const i64 ib = m0 + wr * 32 + 4 * g, jb = n0 + wc * 64 + c;
+    const i64 ib = m0 + wr * WTM + 4 * g, jb = n0 + wc * 64 + c;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < WS::MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
             const i64 j = jb + ni * 16;
@@ -191,12 +198,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32g_kernel(FParams p) {
         }
 }
 
+template <int WTM, bool KCA, bool KCB, bool BUF>
+hipError_t launch_fw(const FParams& p, hipStream_t s) {
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
+    const dim3 block(WaveShape<WTM>::NT);
+    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<WTM, KCA, KCB, true, BUF>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32g_kernel<WTM, KCA, KCB, false, BUF>), grid, block, 0, s, p);
+    return hipGetLastError();
+}
+
 template <bool KCA, bool KCB, bool BUF>
 hipError_t launch_fb(const FParams& p, hipStream_t s) {
-    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, true, BUF>), grid, dim3(NT), 0, s, p);
-    else hipLaunchKernelGGL((gemm_f32g_kernel<KCA, KCB, false, BUF>), grid, dim3(NT), 0, s, p);
-    return hipGetLastError();
+    // 64 x 64 wave tiles (the fp64 kernel's choice) measured a wash here: within
+    // -2 .. +1.7 % of 32 x 64 across shapes (profiles/r01_f32_wave.log)
+    static const int wtm = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 32; }();
+    if (wtm == 64) return launch_fw<64, KCA, KCB, BUF>(p, s);
+    return launch_fw<32, KCA, KCB, BUF>(p, s);
 }
 
 template <bool KCA, bool KCB>
