@@ -58,6 +58,7 @@ _SIGS = {
     "elx_gemm_bf16": (_i, [_i, _i, _i64, _i64, _i64, c_float, _vp, _i64, _vp, _i64, c_float, _vp, _i64, _vp]),
     "elx_axpy2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_copy2d": (_i, [_i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
+    "elx_copy2d_convert": (_i, [_i, _i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_transpose": (_i, [_i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_scale2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _vp]),
     "elx_fill2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _vp]),

@@ -133,6 +133,13 @@ int elx_copy2d(int dtype, int64_t m, int64_t n, const void* A, int64_t acs, int6
         exec::Copy2DBatch(Device::GPU, ToDType(dtype), &d, 1, false, 0.0, S(stream));
     });
 }
+int elx_copy2d_convert(int src_dtype, int dst_dtype, int64_t m, int64_t n, const void* A, int64_t acs, int64_t ars,
+                       void* B, int64_t bcs, int64_t brs, void* stream) {
+    return Guard([&] {
+        kern::Copy2D d{m, n, A, acs, ars, B, bcs, brs};
+        exec::Convert2D(Device::GPU, ToDType(src_dtype), ToDType(dst_dtype), d, S(stream));
+    });
+}
 int elx_transpose(int dtype, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb, void* stream) {
     return Guard([&] {  // B (n x m) = A^T
         kern::Copy2D d{n, m, A, lda, 1, B, 1, ldb};

@@ -115,6 +115,36 @@ void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double
     for (int q = 0; q < nd; ++q) HOST_DTYPE_SWITCH(t, S, cpu_copy<S>(d[q], axpy, alpha));
 }
 
+namespace {
+template <typename TS, typename TD>
+void cpu_convert(const Copy2D& d) {
+    using SS = typename kern::Elem<TS>::storage;
+    using SD = typename kern::Elem<TD>::storage;
+    const SS* src = static_cast<const SS*>(d.src);
+    SD* dst = static_cast<SD*>(d.dst);
+    for (Int j = 0; j < d.n; ++j)
+        for (Int i = 0; i < d.m; ++i)
+            dst[i * d.dcs + j * d.drs] = kern::convert_elem<TS, TD>(src[i * d.scs + j * d.srs]);
+}
+#define KERN_DTYPE_SWITCH(t, T, ...)                                     \
+    switch (t) {                                                         \
+    case DType::F64: { using T = double; __VA_ARGS__; break; }           \
+    case DType::F32: { using T = float; __VA_ARGS__; break; }            \
+    case DType::F16: { using T = kern::f16_t; __VA_ARGS__; break; }      \
+    case DType::BF16: { using T = kern::bf16_t; __VA_ARGS__; break; }    \
+    }
+}  // namespace
+
+void Convert2D(Device dev, DType src_t, DType dst_t, const Copy2D& d, hipStream_t s) {
+    if (d.m <= 0 || d.n <= 0) return;
+    if (src_t == dst_t) { Copy2DBatch(dev, src_t, &d, 1, false, 0.0, s); return; }
+    if (dev == Device::GPU) {
+        check(kern::convert2d(static_cast<int>(src_t), static_cast<int>(dst_t), d, s), "convert2d");
+        return;
+    }
+    KERN_DTYPE_SWITCH(src_t, TS, KERN_DTYPE_SWITCH(dst_t, TD, cpu_convert<TS, TD>(d)));
+}
+
 void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alpha, const void* A, Int lda,
           const void* B, Int ldb, double beta, void* C, Int ldc, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

@@ -14,6 +14,8 @@ namespace exec {
 using kern::Copy2D;
 
 void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
+// dst(i,j) = (dst type) src(i,j): Copy_GPU_impl<SrcT,DestT> (Copy.cu:93-205)
+void Convert2D(Device dev, DType src_t, DType dst_t, const Copy2D& d, hipStream_t s);
 void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alpha,
           const void* A, Int lda, const void* B, Int ldb, double beta, void* C, Int ldc, hipStream_t s);
 void Fill(Device dev, DType t, Int m, Int n, double v, void* A, Int lda, hipStream_t s);

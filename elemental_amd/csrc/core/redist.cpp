@@ -271,7 +271,39 @@ bool SameLocalLayout(const DistMatrix& A, Dist cd, Dist rd, int calign, int rali
     return true;
 }
 
+// El::Copy(ElementalMatrix<S> const& A, DistMatrix<T,U,V>& B) with S != T
+// (include/El/blas_like/level1/CopyDistMatrix.hpp:28-57): when A already has
+// B's distribution, root and (adoptable) alignment, convert the local block in
+// place of a redistribution; otherwise redistribute in S to a temporary aligned
+// with B, then convert locally.
+void CopyConvert(const DistMatrix& A, DistMatrix& B) {
+    ELX_REQUIRE(&A.G() == &B.G(), "matrices live on different grids");
+    const DistMatrix* src = &A;
+    std::shared_ptr<DistMatrix> T;
+    bool direct = false;
+    if (A.ColDist() == B.ColDist() && A.RowDist() == B.RowDist() && A.Dev() == B.Dev() && A.Root() == B.Root()) {
+        if (!B.Viewing()) {
+            if (!B.ColConstrained()) B.AlignCols(A.ColAlign(), false);
+            if (!B.RowConstrained()) B.AlignRows(A.RowAlign(), false);
+        }
+        direct = A.ColAlign() == B.ColAlign() && A.RowAlign() == B.RowAlign();
+    }
+    if (!direct) {
+        T = std::make_shared<DistMatrix>(A.GridPtr(), A.Type(), B.ColDist(), B.RowDist(), B.Dev(), B.Root());
+        T->Align(B.ColAlign(), B.RowAlign(), true);
+        T->SetStream(B.Stream());  // produced, consumed and released on B's stream
+        Copy(A, *T);
+        src = T.get();
+    }
+    B.Resize(A.Height(), A.Width());
+    if (B.LocalHeight() == 0 || B.LocalWidth() == 0) return;
+    Fence(*src, B);
+    kern::Copy2D d{B.LocalHeight(), B.LocalWidth(), src->Buffer(), 1, src->LDim(), B.Buffer(), 1, B.LDim()};
+    exec::Convert2D(B.Dev(), src->Type(), B.Type(), d, B.Stream());
+}
+
 void Copy(const DistMatrix& A, DistMatrix& B) {
+    if (A.Type() != B.Type()) { CopyConvert(A, B); return; }
     CheckCompatible(A, B);
     if (A.Dev() != B.Dev()) {
         auto T = OnDevice(A, B.Dev(), B.Stream());

@@ -36,6 +36,12 @@ struct CopyBatch {
     Copy2D d[kMaxCopyBatch];
 };
 
+template <typename S>
+struct V16 {
+    static constexpr int N = 16 / sizeof(S);
+    S v[N];
+};
+
 template <typename T, bool AXPY>
 __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
     using E = Elem<T>;
@@ -51,6 +57,13 @@ __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
     const bool dst_i = (d.dcs == 1) || (d.drs != 1);
     const int t = threadIdx.x, fast = t & (TILE - 1), slow = t >> 6;
     const Cmp a = (Cmp)alpha;
+    // vector transposition: both operands 16-B aligned along their unit-stride
+    // dimension (base pointer and the other dimension's stride)
+    const i64 es = (i64)sizeof(S);
+    const bool tvec = src_i != dst_i && (reinterpret_cast<uintptr_t>(src) % 16 == 0) &&
+                      (reinterpret_cast<uintptr_t>(dst) % 16 == 0) && (src_i ? d.scs == 1 && (d.srs * es) % 16 == 0
+                                                                               : d.srs == 1 && (d.scs * es) % 16 == 0) &&
+                      (dst_i ? d.dcs == 1 && (d.drs * es) % 16 == 0 : d.drs == 1 && (d.dcs * es) % 16 == 0);
     for (i64 tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
         const i64 i0 = (tile_id % tiles_i) * TILE, j0 = (tile_id / tiles_i) * TILE;
         if (src_i == dst_i) {
@@ -64,6 +77,41 @@ __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
                     S* o = dst + i * d.dcs + j * d.drs;
                     if (AXPY) *o = E::store(E::load(*o) + a * E::load(v));
                     else *o = v;
+                }
+            }
+        } else if (tvec && i0 + TILE <= d.m && j0 + TILE <= d.n) {
+            // transposing, whole tile, 16-B aligned unit-stride runs on both sides:
+            // one 16-B global access per lane (N elements) in and out, the
+            // transposition done element-wise through the LDS tile
+            constexpr int N = V16<S>::N, CH = TILE / N;
+            __syncthreads();
+#pragma unroll
+            for (int v = t; v < TILE * CH; v += NT) {
+                const int c = (v % CH) * N, sl = v / CH;
+                const int li = src_i ? c : sl, lj = src_i ? sl : c;
+                const V16<S> x = *reinterpret_cast<const V16<S>*>(src + (i0 + li) * d.scs + (j0 + lj) * d.srs);
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    if (src_i) tile[lj][li + e] = x.v[e];
+                    else tile[lj + e][li] = x.v[e];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int v = t; v < TILE * CH; v += NT) {
+                const int c = (v % CH) * N, sl = v / CH;
+                const int li = dst_i ? c : sl, lj = dst_i ? sl : c;
+                V16<S>* o = reinterpret_cast<V16<S>*>(dst + (i0 + li) * d.dcs + (j0 + lj) * d.drs);
+                V16<S> x;
+#pragma unroll
+                for (int e = 0; e < N; ++e) x.v[e] = dst_i ? tile[lj][li + e] : tile[lj + e][li];
+                if (AXPY) {
+                    V16<S> y = *o;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) y.v[e] = E::store(E::load(y.v[e]) + a * E::load(x.v[e]));
+                    *o = y;
+                } else {
+                    *o = x;
                 }
             }
         } else {
@@ -91,16 +139,56 @@ __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
     }
 }
 
+// Type-converting strided copy (Copy_GPU_impl<SrcT,DestT>, Copy.cu:93-205):
+// the same two shapes as copy2d_kernel (direct when both sides walk the same
+// unit-stride dimension, LDS-staged 64x64 tile otherwise); the tile holds the
+// converted destination values.
+template <typename TS, typename TD>
+__global__ __launch_bounds__(NT) void convert2d_kernel(Copy2D d) {
+    using SS = typename Elem<TS>::storage;
+    using SD = typename Elem<TD>::storage;
+    __shared__ SD tile[TILE][TILE + 1];  // [j][i]
+    const i64 tiles_i = (d.m + TILE - 1) / TILE, tiles_j = (d.n + TILE - 1) / TILE;
+    const SS* src = static_cast<const SS*>(d.src);
+    SD* dst = static_cast<SD*>(d.dst);
+    const bool src_i = (d.scs == 1) || (d.srs != 1);
+    const bool dst_i = (d.dcs == 1) || (d.drs != 1);
+    const int t = threadIdx.x, fast = t & (TILE - 1), slow = t >> 6;
+    for (i64 tile_id = blockIdx.x; tile_id < tiles_i * tiles_j; tile_id += gridDim.x) {
+        const i64 i0 = (tile_id % tiles_i) * TILE, j0 = (tile_id / tiles_i) * TILE;
+        if (src_i == dst_i) {
+#pragma unroll 4
+            for (int e = 0; e < TILE / 4; ++e) {
+                const i64 i = i0 + (src_i ? fast : slow + 4 * e);
+                const i64 j = j0 + (src_i ? slow + 4 * e : fast);
+                if (i < d.m && j < d.n) dst[i * d.dcs + j * d.drs] = convert_elem<TS, TD>(src[i * d.scs + j * d.srs]);
+            }
+        } else {
+            __syncthreads();
+#pragma unroll 4
+            for (int e = 0; e < TILE / 4; ++e) {
+                const int li = src_i ? fast : slow + 4 * e;
+                const int lj = src_i ? slow + 4 * e : fast;
+                const i64 i = i0 + li, j = j0 + lj;
+                if (i < d.m && j < d.n) tile[lj][li] = convert_elem<TS, TD>(src[i * d.scs + j * d.srs]);
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int e = 0; e < TILE / 4; ++e) {
+                const int li = dst_i ? fast : slow + 4 * e;
+                const int lj = dst_i ? slow + 4 * e : fast;
+                const i64 i = i0 + li, j = j0 + lj;
+                if (i < d.m && j < d.n) dst[i * d.dcs + j * d.drs] = tile[lj][li];
+            }
+        }
+    }
+}
+
 // Vectorized 2-D elementwise engine (HBM-bound ops).  Columns over gridDim.y,
 // rows over gridDim.x*NT lanes, each lane moving VEC = 16 B / sizeof(S)
 // elements per access (one global_load/store_dwordx4) when every operand's
 // column starts are 16-B aligned (uniform per launch); otherwise element by
 // element.  The host collapses contiguous operands (ld == m) into one column.
-template <typename S>
-struct V16 {
-    static constexpr int N = 16 / sizeof(S);
-    S v[N];
-};
 
 // Operand 0 is the output; RD0 says whether the op reads it (scale) or only
 // writes it (fill, hadamard, map), so no HBM read is spent on a pure output.
@@ -178,8 +266,14 @@ __global__ __launch_bounds__(NT) void copy_cols_kernel(CopyBatch b, double alpha
                      ((d.srs * (i64)sizeof(S)) % 16 == 0 || d.n == 1) && ((d.drs * (i64)sizeof(S)) % 16 == 0 || d.n == 1);
     const auto a = (typename E::compute)alpha;
     const i64 mv = (d.m + N - 1) / N, total = mv * d.n;
+    // column of a vector id: 32-bit division when the ids fit (64-bit division is
+    // a long emulated sequence), none at all for a single column
+    const bool one_col = d.n == 1, narrow = total < (1ll << 31);
+    auto col_of = [&](i64 id) -> i64 {
+        return one_col ? 0 : narrow ? (i64)((uint32_t)id / (uint32_t)mv) : id / mv;
+    };
     auto one = [&](i64 id) {
-        const i64 j = id / mv, i = (id - j * mv) * N;
+        const i64 j = col_of(id), i = (id - j * mv) * N;
         const S* x = src + j * d.srs + i;
         S* y = dst + j * d.drs + i;
         if (vec && i + N <= d.m) {
@@ -207,7 +301,7 @@ __global__ __launch_bounds__(NT) void copy_cols_kernel(CopyBatch b, double alpha
             S* y[UNROLL];
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
-                const i64 k = c0 + u * NT + threadIdx.x, j = k / mv, i = (k - j * mv) * N;
+                const i64 k = c0 + u * NT + threadIdx.x, j = col_of(k), i = (k - j * mv) * N;
                 xv[u] = *reinterpret_cast<const V16<S>*>(src + j * d.srs + i);
                 y[u] = dst + j * d.drs + i;
                 if (AXPY) yv[u] = *reinterpret_cast<const V16<S>*>(y[u]);
@@ -393,8 +487,13 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
         bool cols = true;
         const int es = dtype == ELX_F64 ? 8 : dtype == ELX_F32 ? 4 : 2;
         for (int q = 0; q < cnt; ++q) {
-            const Copy2D& x = d[base + q];
+            Copy2D x = d[base + q];
             if (x.m <= 0 || x.n <= 0) continue;
+            if (x.scs == 1 && x.dcs == 1 && x.srs == x.m && x.drs == x.m && x.n > 1) {
+                x.m *= x.n;  // both sides contiguous: one long column
+                x.n = 1;
+                x.srs = x.drs = x.m;
+            }
             b.d[used++] = x;
             const i64 t = ((x.m + TILE - 1) / TILE) * ((x.n + TILE - 1) / TILE);
             if (t > maxtiles) maxtiles = t;
@@ -421,6 +520,15 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t convert2d(int sdt, int ddt, const Copy2D& d, hipStream_t s) {
+    if (d.m <= 0 || d.n <= 0) return hipSuccess;
+    if (sdt == ddt) return copy2d_batch(sdt, &d, 1, false, 0.0, s);
+    const i64 tiles = ((d.m + TILE - 1) / TILE) * ((d.n + TILE - 1) / TILE);
+    const dim3 grid((unsigned)(tiles > 8192 ? 8192 : tiles));
+    ELX_DTYPE_SWITCH(sdt, TS, ELX_DTYPE_SWITCH(ddt, TD, hipLaunchKernelGGL((convert2d_kernel<TS, TD>), grid, dim3(NT), 0, s, d)));
+    return hipGetLastError();
 }
 
 hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s) {

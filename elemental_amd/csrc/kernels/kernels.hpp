@@ -70,6 +70,8 @@ constexpr int kMaxCopyBatch = 16;
 // axpy=false: plain copy (bit-exact, alpha ignored); axpy=true: dst += alpha*src.
 hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
 
+// Type-converting strided copy: dst(i,j) = (dst type) src(i,j), one rounding (elem.hpp).
+hipError_t convert2d(int src_dtype, int dst_dtype, const Copy2D& d, hipStream_t s);
 hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s);
 hipError_t scale2d(int dtype, i64 m, i64 n, double alpha, void* A, i64 lda, hipStream_t s);
 hipError_t hadamard2d(int dtype, i64 m, i64 n, const void* A, i64 lda, const void* B, i64 ldb,

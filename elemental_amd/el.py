@@ -316,6 +316,12 @@ def AxpyContract(alpha, A, B):
     call("elx_dm_axpy_contract", float(alpha), A.h, B.h)
 
 
+def Copy(A: DistMatrix, B: DistMatrix):
+    """B := A (El::Copy): any distribution pair; different element types convert
+    with one rounding (CopyDistMatrix.hpp:28-57)."""
+    call("elx_dm_copy", B.h, A.h)
+
+
 def Transpose(A, B):
     call("elx_dm_transpose", A.h, B.h)
 

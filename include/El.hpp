@@ -258,6 +258,8 @@ void LocalGemm(Orientation orientA, Orientation orientB, T alpha, const Abstract
 
 // ---- level 1 front doors ------------------------------------------------------------
 template <typename T> void Copy(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) { detail::Check(elx_dm_copy(B.h(), A.h())); }
+// S != T: redistribute in S, convert locally (CopyDistMatrix.hpp:28-57)
+template <typename S, typename T> void Copy(const AbstractDistMatrix<S>& A, AbstractDistMatrix<T>& B) { detail::Check(elx_dm_copy(B.h(), A.h())); }
 template <typename T> void Transpose(const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, bool /*conjugate*/ = false) {
     detail::Check(elx_dm_transpose(A.h(), B.h()));
 }

@@ -147,6 +147,12 @@ int elx_axpy2d(int dtype, int64_t m, int64_t n, double alpha,
 int elx_copy2d(int dtype, int64_t m, int64_t n,
                const void* A, int64_t acs, int64_t ars,
                void* B, int64_t bcs, int64_t brs, void* stream);
+/* type-converting copy2d: B(i,j) = (dst_dtype) A(i,j), one round-to-nearest-even
+ * from the exact source value; replaces the SrcT != DestT instantiations of
+ * Copy_GPU_impl (src/hydrogen/blas/gpu/Copy.cu:93-205, ETI :207-244) */
+int elx_copy2d_convert(int src_dtype, int dst_dtype, int64_t m, int64_t n,
+                       const void* A, int64_t acs, int64_t ars,
+                       void* B, int64_t bcs, int64_t brs, void* stream);
 int elx_transpose(int dtype, int64_t m, int64_t n,
                   const void* A, int64_t lda, void* B, int64_t ldb, void* stream);
 int elx_scale2d(int dtype, int64_t m, int64_t n, double alpha,
@@ -235,7 +241,10 @@ int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int
 int elx_dm_attach(elx_dm_t A, int64_t height, int64_t width, int colAlign, int rowAlign,
                   void* buffer, int64_t ldim, int root);
 /* B := A  (DistMatrix::operator=, the redistribution dispatch table,
- * src/core/DistMatrix/ElementMatrix/{MC_MR,MC_STAR,...}.cpp); bit-exact */
+ * src/core/DistMatrix/ElementMatrix/{MC_MR,MC_STAR,...}.cpp); bit-exact.
+ * Different element types: El::Copy(ElementalMatrix<S>, DistMatrix<T>)
+ * (include/El/blas_like/level1/CopyDistMatrix.hpp:28-57) — redistribute in S
+ * to B's distribution and alignment, then convert locally (elx_copy2d_convert). */
 int elx_dm_copy(elx_dm_t B, elx_dm_t A);
 /* B := A^T (El::Transpose, include/El/blas_like/level1/Transpose.hpp:191-250) */
 int elx_dm_transpose(elx_dm_t A, elx_dm_t B);

@@ -136,6 +136,44 @@ def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
     return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
 
 
+# ------------------------------------------------------ type conversion
+# Copy_GPU_impl<SrcT,DestT> (src/hydrogen/blas/gpu/Copy.cu:13-21: `dest = src`):
+# the exact source value rounded once, to nearest-even, into the target format.
+_FMT = {"f32": (24, -126, np.finfo(np.float32).max), "f16": (11, -14, 65504.0),
+        "bf16": (8, -126, float.fromhex("0x1.fep127"))}
+
+
+def round_to_format(d: np.ndarray, fmt: str) -> np.ndarray:
+    """Round float64 values to the `fmt` grid (p significand bits, minimum normal
+    exponent emin, largest finite maxv) by scaling to the quantum of each value's
+    binade and numpy's round-half-even; results stay float64 (exact)."""
+    p, emin, maxv = _FMT[fmt]
+    d = np.asarray(d, dtype=np.float64)
+    _, e = np.frexp(d)                                   # d = m 2^e, 0.5 <= |m| < 1
+    q = np.ldexp(1.0, np.maximum(e, emin + 1) - p)       # quantum (subnormals: 2^(emin+1-p))
+    with np.errstate(over="ignore", invalid="ignore"):
+        r = np.round(d / q) * q
+        r = np.where(np.abs(r) > maxv, np.copysign(np.inf, d), r)
+    return np.where(np.isfinite(d), r, d)
+
+
+def to_f64(x: np.ndarray, fmt: str) -> np.ndarray:
+    """Storage array (bf16 as uint16 bit patterns) -> exact float64 values."""
+    return bf16_bits_to_f32(x).astype(np.float64) if fmt == "bf16" else np.asarray(x).astype(np.float64)
+
+
+def convert(x: np.ndarray, src: str, dst: str) -> np.ndarray:
+    """Type-converting copy of a storage array: src/dst in {f64, f32, f16, bf16}."""
+    d = to_f64(x, src)
+    if dst == "f64":
+        out = d
+    elif dst == "bf16":
+        out = f32_to_bf16_bits(round_to_format(d, "bf16").astype(np.float32))  # exact -> bits
+    else:
+        out = round_to_format(d, dst).astype(np.float32 if dst == "f32" else np.float16)
+    return np.asfortranarray(out)
+
+
 # -------------------------------------------------------------------- gemm
 def gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """C := alpha op(A) op(B) + beta C with the reference's loop nest (f64/f32)."""

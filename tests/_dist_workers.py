@@ -350,3 +350,56 @@ def io_worker(rank: int, world: int, port: int, height: int, device: int, tmpdir
     except Exception:
         traceback.print_exc()
         raise
+
+
+FMT = {0: "f32", 1: "f64", 2: "f16", 3: "bf16"}  # ELX_F32, ELX_F64, ELX_F16, ELX_BF16
+
+
+def convert_values(m: int, n: int, seed: int) -> np.ndarray:
+    """float64 test matrix spanning many binades, with round-to-nearest-even ties
+    of every target format, signed zeros and f16 overflow/underflow."""
+    rng = np.random.default_rng(seed)
+    G = rng.standard_normal((m, n)) * np.ldexp(1.0, rng.integers(-30, 20, (m, n)))
+    special = [1 + 2.0 ** -11, 1 + 3 * 2.0 ** -11, 1 + 2.0 ** -8, 1 + 3 * 2.0 ** -8, 1 + 2.0 ** -24,
+               -(1 + 2.0 ** -8), 0.0, -0.0, 65520.0, 1e6, 2.0 ** -25, 3 * 2.0 ** -26, 1e-30]
+    G.flat[: len(special)] = special
+    return np.asfortranarray(G)
+
+
+def convert_worker(rank: int, world: int, port: int, height: int, device: int, seed: int):
+    """El::Copy(DistMatrix<S>, DistMatrix<T>) for every S != T over a few
+    distribution pairs (same distribution: local conversion; otherwise
+    redistribute in S, then convert), bit-exact against the oracle."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        m, n = 21, 17
+        G = convert_values(m, n, seed)
+        pairs = [((el.MC, el.MR), (el.MC, el.MR)), ((el.MC, el.MR), (el.STAR, el.VR)),
+                 ((el.VC, el.STAR), (el.MC, el.MR)), ((el.CIRC, el.CIRC), (el.MR, el.STAR))]
+        for S in FMT:
+            GS = oracle.convert(G, "f64", FMT[S])
+            for T in FMT:
+                if S == T:
+                    continue
+                want_g = oracle.convert(GS, FMT[S], FMT[T])
+                for (U, V), (X, Y) in pairs:
+                    A = el.DistMatrix(g, S, U, V, device)
+                    A.Resize(m, n)
+                    A.set_local(oracle.local_block(GS, U, V, r, c, g.vc_rank, 0, 0, 0))
+                    for xa in range(min(2, oracle.lib().orc_dist_stride(X, r, c))):
+                        B = el.DistMatrix(g, T, X, Y, device)
+                        B.Align(xa, 0)
+                        el.Copy(A, B)
+                        want = oracle.local_block(want_g, X, Y, r, c, g.vc_rank, xa, 0, 0)
+                        got = B.get_local()
+                        tag = f"{FMT[S]}->{FMT[T]} [{el.DIST_NAMES[X]},{el.DIST_NAMES[Y]}]({xa}) <- " \
+                              f"[{el.DIST_NAMES[U]},{el.DIST_NAMES[V]}] grid {r}x{c} rank {rank}"
+                        assert got.shape == want.shape, f"{tag}: shape {got.shape} vs {want.shape}"
+                        assert np.array_equal(_bits(got), _bits(want)), f"{tag}: data mismatch"
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise

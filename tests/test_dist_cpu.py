@@ -67,3 +67,10 @@ def test_blas1_distributed(world, height):
 def test_write_read_binary(world, height, tmp_path):
     """El::Write / El::Read, BINARY and BINARY_FLAT (src/io/Write.cpp, Read.cpp)."""
     _spawn(W.io_worker, world, height, el.CPU, str(tmp_path))
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_copy_type_conversion(world, height):
+    """El::Copy between element types (CopyDistMatrix.hpp:28-57) on CPU matrices:
+    all 12 ordered pairs of {f32, f64, f16, bf16}, bit-exact vs the oracle."""
+    _spawn(W.convert_worker, world, height, el.CPU, 7)

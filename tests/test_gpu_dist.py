@@ -181,3 +181,9 @@ def test_gpu_set_stream():
     C.set_stream(None)  # back to the library's compute stream
     assert C.stream() == lib_stream
     el.device_synchronize()
+
+
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 2)])
+def test_gpu_copy_type_conversion(world, height):
+    """El::Copy between element types on GPU matrices (convert2d_kernel), bit-exact."""
+    _spawn(W.convert_worker, world, height, el.GPU, 8)

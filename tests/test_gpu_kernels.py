@@ -224,3 +224,34 @@ def test_pool_alloc_free():
     L.call("elx_pool_free", p, None)
     r, u = el.pool_stats()
     assert u == 0 or u >= 0
+
+
+@pytest.mark.parametrize("s", [L.F64, L.F32, L.F16, L.BF16])
+@pytest.mark.parametrize("t", [L.F64, L.F32, L.F16, L.BF16])
+def test_copy2d_convert(s, t):
+    """elx_copy2d_convert (Copy_GPU_impl<SrcT,DestT>): direct, strided and
+    transposing moves, bit-exact vs the oracle's single-rounding restatement."""
+    import _dist_workers as W
+    fs, ft = W.FMT[s], W.FMT[t]
+    hs = np.uint16 if fs == "bf16" else {"f64": np.float64, "f32": np.float32, "f16": np.float16}[fs]
+    ht = np.uint16 if ft == "bf16" else {"f64": np.float64, "f32": np.float32, "f16": np.float16}[ft]
+    m, n = 131, 70
+    X = oracle.convert(W.convert_values(m, n, 3), "f64", fs)
+    dX = dev(X)
+    want = oracle.convert(X, fs, ft)
+    dY = dev(np.zeros((m, n), dtype=ht))
+    L.call("elx_copy2d_convert", s, t, m, n, dX.data_ptr(), 1, m, dY.data_ptr(), 1, m, None)
+    sync()
+    same = lambda a, b: np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
+    assert same(host(dY, (m, n), ht), want)
+    # transposing: Y (n x m) = convert(X^T)
+    dT = dev(np.zeros((n, m), dtype=ht))
+    L.call("elx_copy2d_convert", s, t, n, m, dX.data_ptr(), m, 1, dT.data_ptr(), 1, n, None)
+    sync()
+    assert same(host(dT, (n, m), ht), want.T)
+    # strided: every other row and column
+    mh, nh = (m + 1) // 2, (n + 1) // 2
+    dS = dev(np.zeros((mh, nh), dtype=ht))
+    L.call("elx_copy2d_convert", s, t, mh, nh, dX.data_ptr(), 2, 2 * m, dS.data_ptr(), 1, mh, None)
+    sync()
+    assert same(host(dS, (mh, nh), ht), want[::2, ::2])

@@ -146,3 +146,29 @@ def test_mt_uniform_matches_libstdcxx(tmp_path):
             want = np.array([float(x) for x in out], dtype=np.float64 if kind == "f64" else np.float32)
             got = oracle.mt_uniform(seed, 257, lo, hi, kind)  # (%.9g round-trips a float exactly)
             assert np.array_equal(got, want), (seed, kind)
+
+
+def test_convert_restatement_known_answers():
+    """oracle.convert (Copy_GPU_impl<SrcT,DestT> restated: one round-to-nearest-even
+    from the exact value) agrees with numpy's own correctly rounded f64 -> f16 / f32
+    casts, with a round-to-odd construction for bf16, and with hand-worked ties."""
+    rng = np.random.default_rng(0)
+    d = rng.standard_normal(20000) * 10.0 ** rng.integers(-45, 40, 20000)
+    d = np.concatenate([d, [0.0, -0.0, np.inf, -np.inf, np.nan, 65520.0, 65519.99, 2.0 ** -25, 1.5 * 2.0 ** -24]])
+    with np.errstate(over="ignore"):
+        assert np.array_equal(oracle.convert(d, "f64", "f16").view(np.uint16), d.astype(np.float16).view(np.uint16))
+        assert np.array_equal(oracle.convert(d, "f64", "f32").view(np.uint32), d.astype(np.float32).view(np.uint32))
+        f = d.astype(np.float32)
+    back = f.astype(np.float64)
+    u = f.view(np.uint32).copy()
+    inexact = (back != d) & ~np.isnan(d)
+    u[inexact & (np.abs(back) > np.abs(d))] -= 1
+    u[inexact] |= 1
+    assert np.array_equal(oracle.convert(d, "f64", "bf16"), oracle.f32_to_bf16_bits(u.view(np.float32)))
+    # ties to even, double rounding avoided, overflow to inf
+    ka = {1 + 2.0 ** -8: 0x3F80, 1 + 3 * 2.0 ** -8: 0x3F82, 1 + 2.0 ** -8 + 2.0 ** -30: 0x3F81,
+          float.fromhex("0x1.ff8p127"): 0x7F80, -(1 + 2.0 ** -8): 0xBF80}
+    got = oracle.convert(np.array(list(ka)), "f64", "bf16")
+    assert [int(x) for x in got] == list(ka.values())
+    # f64 -> bf16 via f32 would round 1 + 2^-8 + 2^-30 to the tie 1 + 2^-8 and then to 1.0
+    assert int(oracle.f32_to_bf16_bits(np.array([1 + 2.0 ** -8 + 2.0 ** -30], dtype=np.float32))[0]) == 0x3F80
