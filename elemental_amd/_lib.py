@@ -21,6 +21,7 @@ MC, MD, MR, VC, VR, STAR, CIRC = range(7)
 (GEMM_DEFAULT, GEMM_SUMMA_A_MS, GEMM_SUMMA_A, GEMM_SUMMA_B_MS, GEMM_SUMMA_B, GEMM_SUMMA_C_MS,
  GEMM_SUMMA_C, GEMM_SUMMA_DOT, GEMM_CANNON) = range(9)
 ROW_MAJOR, COLUMN_MAJOR = 0, 1
+LOWER, UPPER = 0, 1  # El::UpperOrLower (include/El/core/types.hpp:511-515)
 CPU, GPU = 0, 1
 F32, F64, F16, BF16 = 0, 1, 2, 3
 (MAP_IDENTITY, MAP_NEGATE, MAP_ABS, MAP_SQUARE, MAP_SQRT, MAP_EXP, MAP_LOG, MAP_RELU, MAP_SIGMOID,
@@ -112,6 +113,8 @@ _SIGS = {
     "elx_dm_axpy_contract": (_i, [_d, _vp, _vp]),
     "elx_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_local_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp]),
+    "elx_syrk": (_i, [_i, _i, _d, _vp, _d, _vp, _i]),
+    "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
     "elx_blocksize": (_i64, []),
     "elx_set_compute_panel": (_i, [_i64]),

@@ -322,6 +322,16 @@ int elx_local_gemm(int oA, int oB, double alpha, elx_dm_t A, elx_dm_t B, double 
                   M(A), M(B), beta, M(C));
     });
 }
+int elx_syrk(int uplo, int orient, double alpha, elx_dm_t A, double beta, elx_dm_t C, int conjugate) {
+    (void)conjugate;  // real types: Herk == Syrk
+    return Guard([&] {
+        CheckOp(orient);
+        Syrk(uplo, orient, alpha, M(A), beta, M(C));
+    });
+}
+int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset) {
+    return Guard([&] { ScaleTrapezoid(alpha, uplo, M(A), offset); });
+}
 int elx_set_blocksize(int64_t nb) { return Guard([&] { SetBlocksize(nb); }); }
 int64_t elx_blocksize(void) { return Blocksize(); }
 int elx_set_compute_panel(int64_t kc) { return Guard([&] { SetComputePanel(kc); }); }

@@ -249,6 +249,29 @@ void Combine(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, 
     });
 }
 
+void Trapezoid(Device dev, DType t, bool lower, Int m, Int n, double alpha, const void* X, Int ldx, double beta,
+               void* Y, Int ldy, Int i0, Int is, Int j0, Int js, Int offset, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) {
+        check(kern::trapezoid2d((int)t, lower, m, n, alpha, X, ldx, beta, Y, ldy, i0, is, j0, js, offset, s),
+              "trapezoid2d");
+        return;
+    }
+    HOST_DTYPE_SWITCH(t, S, {
+        using Cm = typename H<S>::C;
+        const S* x = static_cast<const S*>(X);
+        S* y = static_cast<S*>(Y);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) {
+                const Int gi = i0 + i * is, gj = j0 + j * js - offset;
+                if (lower ? gi < gj : gi > gj) continue;
+                Cm v = (Cm)beta * H<S>::ld(y + i + j * ldy);
+                if (x) v = v + (Cm)alpha * H<S>::ld(x + i + j * ldx);
+                H<S>::st(y + i + j * ldy, v);
+            }
+    });
+}
+
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

@@ -26,6 +26,7 @@
 #include "redist.hpp"
 #include "exec.hpp"
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 namespace elx {
@@ -134,6 +135,105 @@ Int EffectivePanel(const Grid& g, Int K, DType t) {
 }
 
 // ---------------------------------------------------------------------------
+// LocalTrrk (Trrk/Local.hpp:124-300): C_loc += alpha op(a) op(b) on the part of
+// C's local block whose GLOBAL index lies in the lower (gi >= gj) or upper
+// (gi <= gj) triangle.  Local indices map monotonically to global ones, so the
+// triangle is a staircase in local index space.  It is cut recursively (halving
+// the column range): every rectangle entirely inside the triangle is one MFMA
+// GEMM straight into C (beta = 1) - square-ish, large launches - and only the
+// leaves on the diagonal (<= TrrkCols() = 1024 columns, rows rounded out to
+// whole 128-row tiles) are computed into a
+// workspace and folded in by the trapezoid kernel (the reference's "temporary
+// copy" + AxpyTrapezoid, Local.hpp:155-163).  Rows entirely outside are never
+// touched; the wasted FLOPs are half the leaves': ~TrrkCols() / 2n of the update.
+// ---------------------------------------------------------------------------
+constexpr Int kTrrkColsDefault = 1024;
+Int TrrkCols() {  // ELX_TRRK_COLS overrides (tests exercise many ragged leaves)
+    static const Int v = [] {
+        const char* e = getenv("ELX_TRRK_COLS");
+        return e && atoll(e) > 0 ? (Int)atoll(e) : kTrrkColsDefault;
+    }();
+    return v;
+}
+
+Int TrrkRowAlign() {  // ELX_TRRK_ROWS overrides (tests: 1 exercises every rectangle)
+    static const Int v = [] {
+        const char* e = getenv("ELX_TRRK_ROWS");
+        return e && atoll(e) > 0 ? (Int)atoll(e) : Int(128);
+    }();
+    return v;
+}
+
+void TrrkLocal(bool lower, bool ta, bool tb, Int k, double alpha, const void* a, Int lda, const void* b, Int ldb,
+               DistMatrix& C, hipStream_t s, Buffer& tmp) {
+    const Int m = C.LocalHeight(), n = C.LocalWidth();
+    if (m == 0 || n == 0) return;
+    const Int cs = C.ColShift(), cstr = C.ColStride(), rs = C.RowShift(), rstr = C.RowStride();
+    const Device dev = C.Dev();
+    const DType t = C.Type();
+    const size_t es = DTypeSize(t);
+    const Int bw = TrrkCols(), ra = TrrkRowAlign();
+    // local rows whose global row index is < x
+    auto rows_below = [&](Int x) { return x <= cs ? Int(0) : std::min<Int>(m, (x - cs + cstr - 1) / cstr); };
+    auto gcol = [&](Int j) { return rs + j * rstr; };
+    // column j's inside rows: lower [R(j), m), upper [0, R(j))
+    auto R = [&](Int j) { return rows_below(lower ? gcol(j) : gcol(j) + 1); };
+    // rectangle/leaf row boundaries sit on multiples of ra (128: whole MFMA tiles,
+    // 16-B aligned operands, so every rectangle takes the LDS-DMA kernels); the
+    // rows a rounding moves out of a rectangle go to the masked leaf instead
+    auto up = [&](Int i) { return std::min<Int>(m, (i + ra - 1) / ra * ra); };
+    auto down = [&](Int i) { return i / ra * ra; };
+    auto arow = [&](Int i) { return static_cast<const char*>(a) + (ta ? i * lda : i) * es; };
+    auto bcol = [&](Int j) { return static_cast<const char*>(b) + (tb ? j : j * ldb) * es; };
+    auto cptr = [&](Int i, Int j) { return static_cast<char*>(C.Buffer()) + (i + j * C.LDim()) * es; };
+    auto rect = [&](Int i0, Int i1, Int j0, Int j1) {
+        if (i1 > i0 && j1 > j0)
+            exec::Gemm(dev, t, ta, tb, i1 - i0, j1 - j0, k, alpha, arow(i0), lda, bcol(j0), ldb, 1.0, cptr(i0, j0),
+                       C.LDim(), s);
+    };
+    auto leaf = [&](Int i0, Int i1, Int j0, Int j1) {
+        const Int h = i1 - i0, w = j1 - j0;
+        if (h <= 0 || w <= 0) return;
+        const size_t bytes = static_cast<size_t>(h) * w * es;
+        if (tmp.bytes() < bytes) tmp.Reset(dev, bytes, s);
+        exec::Gemm(dev, t, ta, tb, h, w, k, alpha, arow(i0), lda, bcol(j0), ldb, 0.0, tmp.data(), h, s);
+        exec::Trapezoid(dev, t, lower, h, w, 1.0, tmp.data(), h, 1.0, cptr(i0, j0), C.LDim(), cs + i0 * cstr, cstr,
+                        gcol(j0), rstr, 0, s);
+    };
+    // Lower: the strip of columns [j0, j1) is rows [R(j0), end) (rows >= end belong
+    // to an enclosing rectangle; end >= R(j1-1)).  Halving: left columns' rows
+    // [up(R(jm-1)), end) are inside -> rectangle; the rest recurses.
+    std::function<void(Int, Int, Int)> strip_lower = [&](Int j0, Int j1, Int end) {
+        if (j1 - j0 <= bw) return leaf(down(R(j0)), end, j0, j1);
+        const Int jm = j0 + ((j1 - j0 + 1) / 2 + bw - 1) / bw * bw;
+        const Int mid = std::min(end, up(R(jm - 1)));
+        rect(mid, end, j0, jm);
+        strip_lower(j0, jm, mid);
+        strip_lower(jm, j1, end);
+    };
+    // Upper: the strip of columns [j0, j1) is rows [beg, R(j1-1)) (rows < beg belong
+    // to an enclosing rectangle; beg <= R(j0)).  Right columns' rows
+    // [beg, down(R(jm))) are inside -> rectangle; the rest recurses.
+    std::function<void(Int, Int, Int)> strip_upper = [&](Int j0, Int j1, Int beg) {
+        if (j1 - j0 <= bw) return leaf(beg, up(R(j1 - 1)), j0, j1);
+        const Int jm = j0 + ((j1 - j0 + 1) / 2 + bw - 1) / bw * bw;
+        const Int mid = std::max(beg, down(R(jm)));
+        rect(beg, mid, jm, j1);
+        strip_upper(j0, jm, beg);
+        strip_upper(jm, j1, mid);
+    };
+    if (lower) {
+        const Int b0 = up(R(n - 1));  // rows inside for every column
+        rect(b0, m, 0, n);
+        strip_lower(0, n, b0);
+    } else {
+        const Int b0 = down(R(0));
+        rect(0, b0, 0, n);
+        strip_upper(0, n, b0);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // C-stationary SUMMA, all four orientations (NN.hpp:341-385, NT.hpp:251-294,
 // TN.hpp:252-291, TT.hpp:195-240), pipelined over two panel slots.
 //   op(A) panel: NORMAL -> A(:,k) as [MC,*];   TRANSPOSE -> A(k,:) as [*,MC]
@@ -141,8 +241,10 @@ Int EffectivePanel(const Grid& g, Int K, DType t) {
 // ---------------------------------------------------------------------------
 // beta is folded into the first panel's update (the reference scales C in a
 // separate pass first, Gemm.cpp:282; one fewer HBM round trip of C here).
+// uplo >= 0 (Syrk/Herk, Syrk/{LN,LT,UN,UT}.hpp): only C's lower (ELX_LOWER) or
+// upper (ELX_UPPER) triangle is updated, through TrrkLocal.
 void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
-            DistMatrix& CPre) {
+            DistMatrix& CPre, int uplo = -1) {
     auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
@@ -186,6 +288,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         }
     }
     const int np = static_cast<int>((K + kc - 1) / kc);
+    Buffer trrk_tmp;
 
     auto issue = [&](int p) {
         Slot& s = slot[p & 1];
@@ -220,8 +323,12 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             const bool prof = gpu && Prof().on;
             Profiler::Rec rec{};
             if (prof) rec = Prof().Begin(cs);
-            exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(), b.LDim(),
-                       b_p, C.Buffer(), C.LDim(), cs);
+            if (uplo >= 0)
+                TrrkLocal(uplo == ELX_LOWER, !IsN(oA), !IsN(oB), k, alpha, a.Buffer(), a.LDim(), b.Buffer(), b.LDim(),
+                          C, cs, trrk_tmp);
+            else
+                exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(),
+                           b.LDim(), b_p, C.Buffer(), C.LDim(), cs);
             if (prof) Prof().End(rec, cs, 2.0 * m * n * k, Prof().gemm);
         } else if (p == 0) {
             Scale(beta, C);
@@ -516,6 +623,34 @@ void LocalGemmResize(int oA, int oB, double alpha, const DistMatrix& A, const Di
     }
     C.Resize(m, n);
     LocalGemm(oA, oB, alpha, A, B, 0.0, C);
+}
+
+void ScaleTrapezoid(double alpha, int uplo, DistMatrix& A, Int offset) {
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "ScaleTrapezoid: bad UpperOrLower ", uplo);
+    if (alpha == 1.0) return;  // ScaleTrapezoid.hpp:52-53
+    exec::Trapezoid(A.Dev(), A.Type(), uplo == ELX_LOWER, A.LocalHeight(), A.LocalWidth(), 0.0, nullptr, 0, alpha,
+                    A.Buffer(), A.LDim(), A.ColShift(), A.ColStride(), A.RowShift(), A.RowStride(), offset,
+                    A.Stream());
+}
+
+// Syrk / Herk on DistMatrices (src/blas_like/level3/Syrk.cpp:196-211): the
+// trapezoid of C is scaled by beta, then LN/LT/UN/UT run as the C-stationary
+// pipeline with the triangular local update (Syrk/LN.hpp:13-48 and siblings:
+// A1[MC,*] and A1^T[*,MR] per panel, LocalTrrk).  Real types only, so the
+// conjugate flag (Herk) changes nothing.  The reference switches to its Dot
+// variant when width > 10 height (LN.hpp:156); here the panel pipeline serves
+// every shape (same sums, summation order within the normwise tolerance).
+void Syrk(int uplo, int orient, double alpha, const DistMatrix& A, double beta, DistMatrix& C) {
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Syrk: bad UpperOrLower ", uplo);
+    ELX_REQUIRE(orient >= ELX_NORMAL && orient <= ELX_ADJOINT, "Syrk: bad orientation");
+    ELX_REQUIRE(&A.G() == &C.G(), "Syrk: matrices on different grids");
+    ELX_REQUIRE(A.Type() == C.Type(), "Syrk: mixed types");
+    const bool N = orient == ELX_NORMAL;
+    const Int n = N ? A.Height() : A.Width();
+    if (C.Height() != n || C.Width() != n) throw LogicError("Nonconformal Syrk");
+    ScaleTrapezoid(beta, uplo, C, 0);
+    if (N) SummaC(ELX_NORMAL, ELX_TRANSPOSE, alpha, A, A, 1.0, C, uplo);
+    else SummaC(ELX_TRANSPOSE, ELX_NORMAL, alpha, A, A, 1.0, C, uplo);
 }
 
 void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,

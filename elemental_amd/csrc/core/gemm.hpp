@@ -14,6 +14,11 @@ void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatr
 // beta-less form: aligns and resizes C, then beta = 0
 void LocalGemmResize(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, DistMatrix& C);
 
+// A := alpha A on its lower/upper trapezoid (ScaleTrapezoid.hpp:47-88)
+void ScaleTrapezoid(double alpha, int uplo, DistMatrix& A, Int offset);
+// C := alpha op(A) op(A)^T + beta C on C's lower/upper triangle (Syrk.cpp:196-211; Herk for real T)
+void Syrk(int uplo, int orient, double alpha, const DistMatrix& A, double beta, DistMatrix& C);
+
 void SetBlocksize(Int nb);
 Int Blocksize();
 void SetComputePanel(Int kc);

@@ -434,6 +434,28 @@ __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>
     });
 }
 
+// Trapezoid update (ScaleTrapezoid.hpp:47-88, AxpyTrapezoid, LocalTrrk's
+// diagonal blocks in Trrk/Local.hpp:155-210).  Element (i,j) of the local block
+// is global (i0 + i*istride, j0 + j*jstride); inside the trapezoid
+// (lower: gi >= gj - offset, upper: gi <= gj - offset) it becomes
+// beta*Y + alpha*X (X may be null: beta*Y), outside it is neither read nor written.
+template <typename T>
+__global__ __launch_bounds__(NT) void trapezoid_kernel(bool lower, i64 m, i64 n, double alpha,
+                                                       const typename Elem<T>::storage* X, i64 ldx, double beta,
+                                                       typename Elem<T>::storage* Y, i64 ldy, i64 i0, i64 istride,
+                                                       i64 j0, i64 jstride, i64 offset) {
+    using E = Elem<T>;
+    using Cm = typename E::compute;
+    const Cm a = (Cm)alpha, b = (Cm)beta;
+    for_each_2d(m, n, [&](i64 i, i64 j) {
+        const i64 gi = i0 + i * istride, gj = j0 + j * jstride - offset;
+        if (lower ? gi < gj : gi > gj) return;
+        Cm y = b * E::load(Y[i + j * ldy]);
+        if (X) y = y + a * E::load(X[i + j * ldx]);
+        Y[i + j * ldy] = E::store(y);
+    });
+}
+
 // Launch geometry of ew_2d: collapse to one column when every operand is
 // contiguous (ld == m), and decide the 16-B vector path.
 struct EwShape {
@@ -615,6 +637,16 @@ hipError_t fill_hash(int dtype, i64 m, i64 n, void* A, i64 lda, i64 i0, i64 istr
         hipLaunchKernelGGL((hash_kernel<T>), grid2d(m, n), dim3(NT), 0, s, m, n,
                            static_cast<typename Elem<T>::storage*>(A), lda, i0, istride, j0, jstride,
                            seed, center, radius));
+    return hipGetLastError();
+}
+
+hipError_t trapezoid2d(int dtype, bool lower, i64 m, i64 n, double alpha, const void* X, i64 ldx, double beta,
+                       void* Y, i64 ldy, i64 i0, i64 istride, i64 j0, i64 jstride, i64 offset, hipStream_t s) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    ELX_DTYPE_SWITCH(dtype, T,
+        hipLaunchKernelGGL((trapezoid_kernel<T>), grid2d(m, n), dim3(NT), 0, s, lower, m, n, alpha,
+                           static_cast<const typename Elem<T>::storage*>(X), ldx, beta,
+                           static_cast<typename Elem<T>::storage*>(Y), ldy, i0, istride, j0, jstride, offset));
     return hipGetLastError();
 }
 

@@ -82,5 +82,9 @@ hipError_t combine(int dtype, int fn, i64 m, i64 n, const void* A, i64 lda, void
 hipError_t fill_hash(int dtype, i64 m, i64 n, void* A, i64 lda, i64 i0, i64 istride, i64 j0,
                      i64 jstride, uint64_t seed, double center, double radius, hipStream_t s);
 
+// Y(i,j) := beta*Y + alpha*X (X null: beta*Y) where global (i0+i*istride, j0+j*jstride)
+// lies in the lower (gi >= gj - offset) or upper (gi <= gj - offset) trapezoid.
+hipError_t trapezoid2d(int dtype, bool lower, i64 m, i64 n, double alpha, const void* X, i64 ldx, double beta,
+                       void* Y, i64 ldy, i64 i0, i64 istride, i64 j0, i64 jstride, i64 offset, hipStream_t s);
 }  // namespace kern
 }  // namespace elx

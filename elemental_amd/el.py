@@ -17,13 +17,13 @@ from . import _lib as L
 from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_CANNON, GEMM_DEFAULT,
                    GEMM_SUMMA_A, GEMM_SUMMA_A_MS, GEMM_SUMMA_B, GEMM_SUMMA_B_MS, GEMM_SUMMA_C,
                    GEMM_SUMMA_C_MS, GEMM_SUMMA_DOT, GPU, MC, MD, MR, NORMAL, ROW_MAJOR, STAR, TRANSPOSE,
-                   FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT,
+                   FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT, LOWER, UPPER,
                    VC, VR, call, lib)
 
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
-    "Blocksize", "SetComputePanel",
+    "Blocksize", "SetComputePanel", "Syrk", "Herk", "ScaleTrapezoid", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -262,6 +262,22 @@ def Gemm(orientA, orientB, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMat
 
 def LocalGemm(orientA, orientB, alpha, A, B, beta, C):
     call("elx_local_gemm", orientA, orientB, float(alpha), A.h, B.h, float(beta), C.h)
+
+
+def Syrk(uplo, orientation, alpha, A: DistMatrix, beta, C: DistMatrix, conjugate: bool = False):
+    """El::Syrk(uplo, orientation, alpha, A, beta, C, conjugate) (Syrk.cpp:196-211):
+    C := alpha op(A) op(A)^T + beta C on C's uplo triangle; the other triangle is untouched."""
+    call("elx_syrk", uplo, orientation, float(alpha), A.h, float(beta), C.h, int(bool(conjugate)))
+
+
+def Herk(uplo, orientation, alpha, A: DistMatrix, beta, C: DistMatrix):
+    """El::Herk (Herk.cpp): Syrk with conjugation, identical for the real types."""
+    Syrk(uplo, orientation, alpha, A, beta, C, conjugate=True)
+
+
+def ScaleTrapezoid(alpha, uplo, A: DistMatrix, offset: int = 0):
+    """El::ScaleTrapezoid(alpha, uplo, A, offset) (ScaleTrapezoid.hpp:47-88)."""
+    call("elx_dm_scale_trapezoid", float(alpha), uplo, A.h, int(offset))
 
 
 def Axpy(alpha, X: DistMatrix, Y: DistMatrix):

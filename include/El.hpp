@@ -27,6 +27,7 @@ using Int = std::int64_t;
 enum Dist { MC = ELX_MC, MD = ELX_MD, MR = ELX_MR, VC = ELX_VC, VR = ELX_VR, STAR = ELX_STAR, CIRC = ELX_CIRC };
 enum DistWrap { ELEMENT = 0, BLOCK = 1 };
 enum Orientation { NORMAL = ELX_NORMAL, TRANSPOSE = ELX_TRANSPOSE, ADJOINT = ELX_ADJOINT };
+enum UpperOrLower { LOWER = ELX_LOWER, UPPER = ELX_UPPER };
 enum GridOrder { ROW_MAJOR = ELX_ROW_MAJOR, COLUMN_MAJOR = ELX_COLUMN_MAJOR };
 enum GemmAlgorithm {
     GEMM_DEFAULT = ELX_GEMM_DEFAULT, GEMM_SUMMA_A_MS = ELX_GEMM_SUMMA_A_MS, GEMM_SUMMA_A = ELX_GEMM_SUMMA_A,
@@ -254,6 +255,30 @@ template <typename T>
 void LocalGemm(Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
                const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
     detail::Check(elx_local_gemm(orientA, orientB, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h()));
+}
+// Syrk / Herk (src/blas_like/level3/Syrk.cpp:196-225): C's uplo triangle only
+template <typename T>
+void Syrk(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A, T beta,
+          AbstractDistMatrix<T>& C, bool conjugate = false) {
+    detail::Check(elx_syrk(uplo, orientation, detail::ToDouble(alpha), A.h(), detail::ToDouble(beta), C.h(), conjugate));
+}
+// beta-less form: C resized to n x n and zeroed first (Syrk.cpp:213-225)
+template <typename T>
+void Syrk(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A,
+          AbstractDistMatrix<T>& C, bool conjugate = false) {
+    const Int n = orientation == NORMAL ? A.Height() : A.Width();
+    C.Resize(n, n);
+    detail::Check(elx_dm_zero(C.h()));
+    detail::Check(elx_syrk(uplo, orientation, detail::ToDouble(alpha), A.h(), 0.0, C.h(), conjugate));
+}
+template <typename T>
+void Herk(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A, T beta,
+          AbstractDistMatrix<T>& C) {
+    Syrk(uplo, orientation, alpha, A, beta, C, true);
+}
+template <typename T>
+void ScaleTrapezoid(T alpha, UpperOrLower uplo, AbstractDistMatrix<T>& A, Int offset = 0) {
+    detail::Check(elx_dm_scale_trapezoid(detail::ToDouble(alpha), uplo, A.h(), offset));
 }
 
 // ---- level 1 front doors ------------------------------------------------------------

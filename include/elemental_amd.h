@@ -52,6 +52,9 @@ extern "C" {
 #define ELX_GEMM_SUMMA_C    6
 #define ELX_GEMM_SUMMA_DOT  7
 #define ELX_GEMM_CANNON     8
+/* El::UpperOrLower  include/El/core/types.hpp:511-515 */
+#define ELX_LOWER 0
+#define ELX_UPPER 1
 /* El::GridOrder  include/El/core/types.hpp:408-413 */
 #define ELX_ROW_MAJOR    0
 #define ELX_COLUMN_MAJOR 1
@@ -292,6 +295,13 @@ int elx_gemm(int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t B,
              double beta, elx_dm_t C, int alg);
 int elx_local_gemm(int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t B,
                    double beta, elx_dm_t C);
+/* El::Syrk / El::Herk on DistMatrices (src/blas_like/level3/Syrk.cpp:196-225,
+ * Herk.cpp): C := alpha op(A) op(A)^T + beta C on C's uplo triangle only; the
+ * other triangle is neither read nor written.  conjugate (Herk) is a no-op for
+ * the real types. */
+int elx_syrk(int uplo, int orient, double alpha, elx_dm_t A, double beta, elx_dm_t C, int conjugate);
+/* A := alpha A on its uplo trapezoid (include/El/blas_like/level1/ScaleTrapezoid.hpp:47-88) */
+int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset);
 /* Blocksize stack (src/core/environment.cpp:315: default 128) */
 int elx_set_blocksize(int64_t nb);
 int64_t elx_blocksize(void);

@@ -188,6 +188,21 @@ def gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndar
     return C
 
 
+def syrk(uplo: str, trans: str, alpha, A: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """C := alpha op(A) op(A)^T + beta C on C's uplo ('L'/'U') triangle only, the
+    rest of C untouched: BLAS xSYRK semantics, which the reference's CPU path calls
+    (Syrk.cpp:20-41 -> blas::Syrk) and its distributed Syrk reproduces
+    (Syrk.cpp:196-211: ScaleTrapezoid(beta) then LocalTrrk per panel).  The full
+    product comes from the reference GEMM loop nest above."""
+    full = gemm(trans, "T" if trans == "N" else "N", alpha, A, A, beta, C)
+    n = C.shape[0]
+    i, j = np.indices((n, n))
+    mask = (i >= j) if uplo == "L" else (i <= j)
+    out = np.array(C, order="F", copy=True)
+    out[mask] = full[mask]
+    return out
+
+
 def cpu_gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """bench.py's CPU baseline: blocked OpenMP f64 GEMM (cpu_gemm.c), BLAS semantics."""
     C = np.array(C, order="F", copy=True, dtype=np.float64)

@@ -132,6 +132,53 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         raise
 
 
+def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, nb: int,
+                seed: int):
+    """El::Syrk/Herk, LOWER/UPPER x NORMAL/TRANSPOSE (Syrk/{LN,LT,UN,UT}.hpp): the
+    uplo triangle against oracle.syrk (north_star tolerance), the other triangle
+    bit-identical to the input (including NaNs planted there)."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = np.float64 if dtype == el.F64 else np.float32
+        el.SetBlocksize(nb)
+        for (n, k) in shapes:
+            for uplo in (el.LOWER, el.UPPER):
+                for orient in (el.NORMAL, el.TRANSPOSE):
+                    Ag = oracle.hash_matrix(n if orient == 0 else k, k if orient == 0 else n, seed + 1, -0.1, 0.1,
+                                            npdt)
+                    Cg = oracle.hash_matrix(n, n, seed + 3, -0.1, 0.1, npdt)
+                    i, j = np.indices((n, n))
+                    outside = (i < j) if uplo == el.LOWER else (i > j)
+                    Cg[outside & ((i + j) % 3 == 0)] = np.nan  # never read
+                    alpha, beta = 0.5, -0.5
+                    ref = oracle.syrk("L" if uplo == el.LOWER else "U", ORIENTS[orient], alpha, Ag, beta, Cg)
+                    A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Ag.shape[0], width=Ag.shape[1])
+                    C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=n, width=n)
+                    A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+                    C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                    if (uplo + orient) % 2:
+                        el.Herk(uplo, orient, alpha, A, beta, C)
+                    else:
+                        el.Syrk(uplo, orient, alpha, A, beta, C)
+                    got = C.get_local()
+                    want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank)
+                    out_loc = oracle.local_block(outside.astype(np.uint8), el.MC, el.MR, r, c, g.vc_rank).astype(bool)
+                    assert np.array_equal(_bits(got[out_loc]), _bits(want[out_loc])), \
+                        f"Syrk uplo {uplo} orient {orient} touched the other triangle (rank {rank})"
+                    d = (got.astype(np.float64) - want.astype(np.float64))[~out_loc]
+                    num = np.linalg.norm(d) if d.size else 0.0
+                    den = np.linalg.norm(Ag.astype(np.float64)) ** 2 * max(k, 1) * _tol(dtype)
+                    assert num <= 10 * den, (f"Syrk uplo {uplo} orient {orient} n={n} k={k} grid {r}x{c} "
+                                             f"rank {rank}: {num / den:.3g}")
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 def cannon_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, seed: int):
     """Cannon_NN (src/blas_like/level3/Gemm/NN.hpp:21-104) on a square grid with
     misaligned A, B and C (exercises the initial skew shifts), against the

@@ -45,6 +45,16 @@ def test_gemm_f32_grid_2x2():
     _spawn(W.gemm_worker, 4, 2, el.CPU, el.F32, [(17, 21, 15)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 4, 11)
 
 
+@pytest.mark.parametrize("world,height,cols", [(1, 1, 0), (2, 1, 0), (4, 2, 0), (1, 1, 3), (4, 2, 2), (2, 2, 5)])
+def test_syrk_herk(world, height, cols, monkeypatch):
+    """El::Syrk / El::Herk LN/LT/UN/UT on 1x1, 1x2, 2x1 and 2x2 grids (Syrk/*.hpp);
+    cols > 0 cuts the local triangular update into many ragged column blocks."""
+    if cols:
+        monkeypatch.setenv("ELX_TRRK_COLS", str(cols))
+        monkeypatch.setenv("ELX_TRRK_ROWS", str(1 + cols % 3))
+    _spawn(W.syrk_worker, world, height, el.CPU, el.F64, [(23, 9), (7, 30)], 4, 17)
+
+
 @pytest.mark.parametrize("world,height", [(1, 1), (4, 2), (2, 1)])
 def test_gemm_cannon(world, height):
     """Cannon_NN on 1x1 and 2x2 with random alignments; LogicError on a 2x1 grid,

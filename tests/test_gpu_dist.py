@@ -187,3 +187,41 @@ def test_gpu_set_stream():
 def test_gpu_copy_type_conversion(world, height):
     """El::Copy between element types on GPU matrices (convert2d_kernel), bit-exact."""
     _spawn(W.convert_worker, world, height, el.GPU, 8)
+
+
+@pytest.mark.parametrize("world,height,cols", [(1, 1, 0), (2, 1, 0), (4, 2, 3)])
+def test_gpu_syrk_distributed(world, height, cols, monkeypatch):
+    """El::Syrk / El::Herk LN/LT/UN/UT through the GPU pipeline and the trapezoid
+    kernel (host-staged ranks on one device); cols > 0: many ragged column blocks."""
+    if cols:
+        monkeypatch.setenv("ELX_TRRK_COLS", str(cols))
+        monkeypatch.setenv("ELX_TRRK_ROWS", "2")
+    _spawn(W.syrk_worker, world, height, el.GPU, el.F64, [(45, 19), (16, 70)], 16, 21)
+
+
+@pytest.mark.parametrize("dtype", [el.F64, el.F32])
+def test_gpu_syrk_large(dtype):
+    """1x1 grid, n = 2500 (five 512-column blocks, a ragged last one), k = 640:
+    every uplo x orientation against a float64 numpy product, the other triangle
+    bit-identical to its input."""
+    n, k = 2500, 640
+    npdt = np.float64 if dtype == el.F64 else np.float32
+    eps = np.finfo(npdt).eps
+    g = el.Grid()
+    i, j = np.indices((n, n))
+    for uplo in (el.LOWER, el.UPPER):
+        for orient in (el.NORMAL, el.TRANSPOSE):
+            shape = (n, k) if orient == el.NORMAL else (k, n)
+            A = el.DistMatrix(g, dtype, height=shape[0], width=shape[1]).fill_hash(11, -0.1, 0.1)
+            C = el.DistMatrix(g, dtype, height=n, width=n).fill_hash(12, -0.1, 0.1)
+            el.Syrk(uplo, orient, 0.5, A, -0.5, C)
+            got = C.get_local()
+            Ag = oracle.hash_matrix(*shape, 11, -0.1, 0.1, npdt).astype(np.float64)
+            Cg = oracle.hash_matrix(n, n, 12, -0.1, 0.1, npdt)
+            P = Ag @ Ag.T if orient == el.NORMAL else Ag.T @ Ag
+            inside = (i >= j) if uplo == el.LOWER else (i <= j)
+            assert np.array_equal(got[~inside], Cg[~inside])
+            ref = 0.5 * P - 0.5 * Cg.astype(np.float64)
+            num = np.linalg.norm((got.astype(np.float64) - ref)[inside])
+            den = np.linalg.norm(Ag) ** 2 * k * eps
+            assert num <= 10 * den, (uplo, orient, num / den)
