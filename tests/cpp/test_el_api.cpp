@@ -71,6 +71,25 @@ int main() {
         }
     EXPECT(err <= 1e-12);
 
+    // Syrk (beta-less): E := tril(A^T A); its strict upper triangle stays zero
+    El::DistMatrix<double> E(g);
+    El::Syrk(El::LOWER, El::TRANSPOSE, 1.0, A, E);
+    EXPECT(E.Height() == k && E.Width() == k);
+    auto e = Local(E);
+    err = 0;
+    for (Int j = 0; j < k; ++j)
+        for (Int i = 0; i < k; ++i)
+            err = std::max(err, std::fabs(e[i + j * k] - (i >= j ? d[i + j * k] : 0.0)));
+    EXPECT(err <= 1e-12);
+    // Herk with beta: the upper triangle is scaled and updated, the lower untouched
+    El::Herk(El::UPPER, El::TRANSPOSE, 1.0, A, 2.0, E);
+    e = Local(E);
+    err = 0;
+    for (Int j = 0; j < k; ++j)
+        for (Int i = 0; i < k; ++i)
+            err = std::max(err, std::fabs(e[i + j * k] - (i > j ? d[i + j * k] : i == j ? 3.0 * d[i + j * k] : d[i + j * k])));
+    EXPECT(err <= 1e-12);
+
     // redistribution + transpose + view are bit-exact
     El::DistMatrix<double, El::STAR, El::STAR> S(A);
     EXPECT(Local(S) == a);
