@@ -114,6 +114,8 @@ _SIGS = {
     "elx_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_local_gemm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp]),
     "elx_syrk": (_i, [_i, _i, _d, _vp, _d, _vp, _i]),
+    "elx_trrk": (_i, [_i, _i, _i, _d, _vp, _vp, _d, _vp]),
+    "elx_syr2k": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
     "elx_blocksize": (_i64, []),

@@ -329,6 +329,20 @@ int elx_syrk(int uplo, int orient, double alpha, elx_dm_t A, double beta, elx_dm
         Syrk(uplo, orient, alpha, M(A), beta, M(C));
     });
 }
+int elx_trrk(int uplo, int oA, int oB, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C) {
+    return Guard([&] {
+        CheckOp(oA);
+        CheckOp(oB);
+        Trrk(uplo, oA, oB, alpha, M(A), M(B), beta, M(C));
+    });
+}
+int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C, int conjugate) {
+    (void)conjugate;  // real types: Her2k == Syr2k
+    return Guard([&] {
+        CheckOp(orient);
+        Syr2k(uplo, orient, alpha, M(A), M(B), beta, M(C));
+    });
+}
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset) {
     return Guard([&] { ScaleTrapezoid(alpha, uplo, M(A), offset); });
 }

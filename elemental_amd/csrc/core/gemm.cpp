@@ -653,6 +653,43 @@ void Syrk(int uplo, int orient, double alpha, const DistMatrix& A, double beta, 
     else SummaC(ELX_TRANSPOSE, ELX_NORMAL, alpha, A, A, 1.0, C, uplo);
 }
 
+// Trrk on DistMatrices (src/blas_like/level3/Trrk.cpp:100-117): C := alpha op(A)
+// op(B) + beta C on C's uplo triangle; TrrkNN/NT/TN/TT are the same C-stationary
+// pipeline with the triangular local update.
+void Trrk(int uplo, int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
+          DistMatrix& C) {
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Trrk: bad UpperOrLower ", uplo);
+    ELX_REQUIRE(&A.G() == &B.G() && &A.G() == &C.G(), "Trrk: matrices on different grids");
+    ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "Trrk: mixed types");
+    if (oA == ELX_ADJOINT) oA = ELX_TRANSPOSE;
+    if (oB == ELX_ADJOINT) oB = ELX_TRANSPOSE;
+    const Int m = IsN(oA) ? A.Height() : A.Width(), k = IsN(oA) ? A.Width() : A.Height();
+    const Int kb = IsN(oB) ? B.Height() : B.Width(), n = IsN(oB) ? B.Width() : B.Height();
+    if (m != C.Height() || n != C.Width() || k != kb || m != n) throw LogicError("Nonconformal Trrk");
+    ScaleTrapezoid(beta, uplo, C, 0);
+    SummaC(oA, oB, alpha, A, B, 1.0, C, uplo);
+}
+
+// Syr2k / Her2k (src/blas_like/level3/Syr2k.cpp:78-93, Syr2k/LN.hpp): C := alpha
+// (op(A) op(B)^T + op(B) op(A)^T) + beta C on C's uplo triangle.  The reference
+// gathers both panels and runs two LocalTrrks per panel; here each term is one
+// pass of the triangular pipeline.  Real types: conj(alpha) = alpha.
+void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
+           DistMatrix& C) {
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Syr2k: bad UpperOrLower ", uplo);
+    ELX_REQUIRE(orient >= ELX_NORMAL && orient <= ELX_ADJOINT, "Syr2k: bad orientation");
+    ELX_REQUIRE(&A.G() == &B.G() && &A.G() == &C.G(), "Syr2k: matrices on different grids");
+    ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "Syr2k: mixed types");
+    const bool N = orient == ELX_NORMAL;
+    const Int n = N ? A.Height() : A.Width();
+    if (A.Height() != B.Height() || A.Width() != B.Width() || C.Height() != n || C.Width() != n)
+        throw LogicError("Nonconformal Syr2k");
+    ScaleTrapezoid(beta, uplo, C, 0);
+    const int oA = N ? ELX_NORMAL : ELX_TRANSPOSE, oB = N ? ELX_TRANSPOSE : ELX_NORMAL;
+    SummaC(oA, oB, alpha, A, B, 1.0, C, uplo);
+    SummaC(oA, oB, alpha, B, A, 1.0, C, uplo);
+}
+
 void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,
           int alg) {
     ELX_REQUIRE(oA >= ELX_NORMAL && oA <= ELX_ADJOINT && oB >= ELX_NORMAL && oB <= ELX_ADJOINT, "bad orientation");

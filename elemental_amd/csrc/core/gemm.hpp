@@ -18,6 +18,12 @@ void LocalGemmResize(int oA, int oB, double alpha, const DistMatrix& A, const Di
 void ScaleTrapezoid(double alpha, int uplo, DistMatrix& A, Int offset);
 // C := alpha op(A) op(A)^T + beta C on C's lower/upper triangle (Syrk.cpp:196-211; Herk for real T)
 void Syrk(int uplo, int orient, double alpha, const DistMatrix& A, double beta, DistMatrix& C);
+// C := alpha op(A) op(B) + beta C on C's uplo triangle (Trrk.cpp:100-117)
+void Trrk(int uplo, int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
+          DistMatrix& C);
+// C := alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on C's uplo triangle (Syr2k.cpp:78-93)
+void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
+           DistMatrix& C);
 
 void SetBlocksize(Int nb);
 Int Blocksize();

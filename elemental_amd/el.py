@@ -23,7 +23,7 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
-    "Blocksize", "SetComputePanel", "Syrk", "Herk", "ScaleTrapezoid", "LOWER", "UPPER",
+    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "ScaleTrapezoid", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -273,6 +273,21 @@ def Syrk(uplo, orientation, alpha, A: DistMatrix, beta, C: DistMatrix, conjugate
 def Herk(uplo, orientation, alpha, A: DistMatrix, beta, C: DistMatrix):
     """El::Herk (Herk.cpp): Syrk with conjugation, identical for the real types."""
     Syrk(uplo, orientation, alpha, A, beta, C, conjugate=True)
+
+
+def Trrk(uplo, orientA, orientB, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix):
+    """El::Trrk(uplo, orientA, orientB, alpha, A, B, beta, C) (Trrk.cpp:100-117)."""
+    call("elx_trrk", uplo, orientA, orientB, float(alpha), A.h, B.h, float(beta), C.h)
+
+
+def Syr2k(uplo, orientation, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix, conjugate: bool = False):
+    """El::Syr2k (Syr2k.cpp:78-93): C := alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on uplo."""
+    call("elx_syr2k", uplo, orientation, float(alpha), A.h, B.h, float(beta), C.h, int(bool(conjugate)))
+
+
+def Her2k(uplo, orientation, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix):
+    """El::Her2k: Syr2k with conjugation, identical for the real types."""
+    Syr2k(uplo, orientation, alpha, A, B, beta, C, conjugate=True)
 
 
 def ScaleTrapezoid(alpha, uplo, A: DistMatrix, offset: int = 0):

@@ -277,6 +277,22 @@ void Herk(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDis
     Syrk(uplo, orientation, alpha, A, beta, C, true);
 }
 template <typename T>
+void Trrk(UpperOrLower uplo, Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
+          const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
+    detail::Check(elx_trrk(uplo, orientA, orientB, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h()));
+}
+template <typename T>
+void Syr2k(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A,
+           const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C, bool conjugate = false) {
+    detail::Check(elx_syr2k(uplo, orientation, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h(),
+                            conjugate));
+}
+template <typename T>
+void Her2k(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A,
+           const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
+    Syr2k(uplo, orientation, alpha, A, B, beta, C, true);
+}
+template <typename T>
 void ScaleTrapezoid(T alpha, UpperOrLower uplo, AbstractDistMatrix<T>& A, Int offset = 0) {
     detail::Check(elx_dm_scale_trapezoid(detail::ToDouble(alpha), uplo, A.h(), offset));
 }

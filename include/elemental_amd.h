@@ -300,6 +300,14 @@ int elx_local_gemm(int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t 
  * other triangle is neither read nor written.  conjugate (Herk) is a no-op for
  * the real types. */
 int elx_syrk(int uplo, int orient, double alpha, elx_dm_t A, double beta, elx_dm_t C, int conjugate);
+/* El::Trrk (src/blas_like/level3/Trrk.cpp:100-117): C := alpha op(A) op(B) + beta C
+ * on C's uplo triangle only */
+int elx_trrk(int uplo, int orientA, int orientB, double alpha, elx_dm_t A, elx_dm_t B,
+             double beta, elx_dm_t C);
+/* El::Syr2k / El::Her2k (src/blas_like/level3/Syr2k.cpp:78-105, Her2k.cpp):
+ * C := alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on C's uplo triangle */
+int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double beta,
+              elx_dm_t C, int conjugate);
 /* A := alpha A on its uplo trapezoid (include/El/blas_like/level1/ScaleTrapezoid.hpp:47-88) */
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset);
 /* Blocksize stack (src/core/environment.cpp:315: default 128) */

@@ -203,6 +203,32 @@ def syrk(uplo: str, trans: str, alpha, A: np.ndarray, beta, C: np.ndarray) -> np
     return out
 
 
+def _tri_mask(n: int, uplo: str) -> np.ndarray:
+    i, j = np.indices((n, n))
+    return (i >= j) if uplo == "L" else (i <= j)
+
+
+def trrk(uplo: str, ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """El::Trrk (Trrk.cpp:100-117, Trrk/Local.hpp): the GEMM update applied to C's
+    uplo triangle only (ScaleTrapezoid(beta) + LocalTrrk per panel)."""
+    full = gemm(ta, tb, alpha, A, B, beta, C)
+    out = np.array(C, order="F", copy=True)
+    mask = _tri_mask(C.shape[0], uplo)
+    out[mask] = full[mask]
+    return out
+
+
+def syr2k(uplo: str, trans: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """BLAS xSYR2K semantics (Syr2k.cpp:20-40 -> blas::Syr2k; distributed
+    Syr2k.cpp:78-93): alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on uplo."""
+    tb = "T" if trans == "N" else "N"
+    full = gemm(trans, tb, alpha, B, A, 1.0, gemm(trans, tb, alpha, A, B, beta, C))
+    out = np.array(C, order="F", copy=True)
+    mask = _tri_mask(C.shape[0], uplo)
+    out[mask] = full[mask]
+    return out
+
+
 def cpu_gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """bench.py's CPU baseline: blocked OpenMP f64 GEMM (cpu_gemm.c), BLAS semantics."""
     C = np.array(C, order="F", copy=True, dtype=np.float64)

@@ -134,9 +134,10 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
 
 def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, nb: int,
                 seed: int):
-    """El::Syrk/Herk, LOWER/UPPER x NORMAL/TRANSPOSE (Syrk/{LN,LT,UN,UT}.hpp): the
-    uplo triangle against oracle.syrk (north_star tolerance), the other triangle
-    bit-identical to the input (including NaNs planted there)."""
+    """El::Syrk/Herk, Syr2k/Her2k and Trrk, LOWER/UPPER x NORMAL/TRANSPOSE
+    (Syrk/*.hpp, Syr2k/*.hpp, Trrk/*.hpp): the uplo triangle against the oracle
+    (north_star tolerance), the other triangle bit-identical to the input
+    (including NaNs planted there)."""
     import oracle
     el, comm = init(rank, world, port)
     try:
@@ -173,6 +174,40 @@ def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
                     den = np.linalg.norm(Ag.astype(np.float64)) ** 2 * max(k, 1) * _tol(dtype)
                     assert num <= 10 * den, (f"Syrk uplo {uplo} orient {orient} n={n} k={k} grid {r}x{c} "
                                              f"rank {rank}: {num / den:.3g}")
+
+                    # Syr2k / Her2k with a second operand of A's shape
+                    Bg = oracle.hash_matrix(*Ag.shape, seed + 2, -0.1, 0.1, npdt)
+                    ref2 = oracle.syr2k("L" if uplo == el.LOWER else "U", ORIENTS[orient], alpha, Ag, Bg, beta, Cg)
+                    B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Bg.shape[0], width=Bg.shape[1])
+                    B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
+                    C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                    (el.Her2k if orient else el.Syr2k)(uplo, orient, alpha, A, B, beta, C)
+                    got = C.get_local()
+                    want = oracle.local_block(ref2, el.MC, el.MR, r, c, g.vc_rank)
+                    assert np.array_equal(_bits(got[out_loc]), _bits(want[out_loc])), "Syr2k touched the other triangle"
+                    d = (got.astype(np.float64) - want.astype(np.float64))[~out_loc]
+                    num = np.linalg.norm(d) if d.size else 0.0
+                    den = 2 * np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) \
+                        * max(k, 1) * _tol(dtype)
+                    assert num <= 10 * den, f"Syr2k uplo {uplo} orient {orient} rank {rank}: {num / den:.3g}"
+
+                    # Trrk with mixed orientations: op(A) n x k, op(B) k x n
+                    oB = (orient + uplo) % 2
+                    Tg = oracle.hash_matrix(k if oB == 0 else n, n if oB == 0 else k, seed + 4, -0.1, 0.1, npdt)
+                    ref3 = oracle.trrk("L" if uplo == el.LOWER else "U", ORIENTS[orient], ORIENTS[oB], alpha,
+                                       Ag, Tg, beta, Cg)
+                    T = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Tg.shape[0], width=Tg.shape[1])
+                    T.set_local(oracle.local_block(Tg, el.MC, el.MR, r, c, g.vc_rank))
+                    C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                    el.Trrk(uplo, orient, oB, alpha, A, T, beta, C)
+                    got = C.get_local()
+                    want = oracle.local_block(ref3, el.MC, el.MR, r, c, g.vc_rank)
+                    assert np.array_equal(_bits(got[out_loc]), _bits(want[out_loc])), "Trrk touched the other triangle"
+                    d = (got.astype(np.float64) - want.astype(np.float64))[~out_loc]
+                    num = np.linalg.norm(d) if d.size else 0.0
+                    den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Tg.astype(np.float64)) \
+                        * max(k, 1) * _tol(dtype)
+                    assert num <= 10 * den, f"Trrk uplo {uplo} oA {orient} oB {oB} rank {rank}: {num / den:.3g}"
         finish()
     except Exception:
         traceback.print_exc()
