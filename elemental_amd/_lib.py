@@ -22,6 +22,8 @@ MC, MD, MR, VC, VR, STAR, CIRC = range(7)
  GEMM_SUMMA_C, GEMM_SUMMA_DOT, GEMM_CANNON) = range(9)
 ROW_MAJOR, COLUMN_MAJOR = 0, 1
 LOWER, UPPER = 0, 1  # El::UpperOrLower (include/El/core/types.hpp:511-515)
+LEFT, RIGHT = 0, 1  # El::LeftOrRight (types.hpp:418-422)
+NON_UNIT, UNIT = 0, 1  # El::UnitOrNonUnit (types.hpp:489-493)
 CPU, GPU = 0, 1
 F32, F64, F16, BF16 = 0, 1, 2, 3
 (MAP_IDENTITY, MAP_NEGATE, MAP_ABS, MAP_SQUARE, MAP_SQRT, MAP_EXP, MAP_LOG, MAP_RELU, MAP_SIGMOID,
@@ -116,6 +118,7 @@ _SIGS = {
     "elx_syrk": (_i, [_i, _i, _d, _vp, _d, _vp, _i]),
     "elx_trrk": (_i, [_i, _i, _i, _d, _vp, _vp, _d, _vp]),
     "elx_syr2k": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
+    "elx_trsm": (_i, [_i, _i, _i, _i, _d, _vp, _vp]),
     "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
     "elx_blocksize": (_i64, []),

@@ -343,6 +343,12 @@ int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double
         Syr2k(uplo, orient, alpha, M(A), M(B), beta, M(C));
     });
 }
+int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B) {
+    return Guard([&] {
+        CheckOp(orient);
+        Trsm(side, uplo, orient, diag, alpha, M(A), M(B));
+    });
+}
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset) {
     return Guard([&] { ScaleTrapezoid(alpha, uplo, M(A), offset); });
 }

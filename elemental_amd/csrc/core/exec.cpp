@@ -272,6 +272,39 @@ void Trapezoid(Device dev, DType t, bool lower, Int m, Int n, double alpha, cons
     });
 }
 
+template <typename S>
+void cpu_trsm(bool lower, bool trans, bool unit, Int m, Int n, const S* A, Int lda, S* B, Int ldb) {
+    const bool forward = lower != trans;
+    auto opA = [&](Int r, Int c) { return trans ? A[c + r * lda] : A[r + c * lda]; };
+    for (Int j = 0; j < n; ++j) {
+        S* x = B + j * ldb;
+        for (Int s = 0; s < m; ++s) {
+            const Int i = forward ? s : m - 1 - s;
+            S xi = x[i];
+            if (!unit) xi = xi / opA(i, i);
+            x[i] = xi;
+            if (forward)
+                for (Int r = i + 1; r < m; ++r) x[r] = x[r] - opA(r, i) * xi;
+            else
+                for (Int r = 0; r < i; ++r) x[r] = x[r] - opA(r, i) * xi;
+        }
+    }
+}
+
+void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, const void* A, Int lda, void* B,
+          Int ldb, hipStream_t s) {
+    if (t != DType::F64 && t != DType::F32) throw LogicError("Trsm: only float and double are supported");
+    if (m <= 0 || n <= 0) return;
+    if (dev == Device::GPU) {
+        check(kern::trsm_local((int)t, lower, trans, unit, m, n, A, lda, B, ldb, s), "trsm_local");
+        return;
+    }
+    if (t == DType::F64)
+        cpu_trsm(lower, trans, unit, m, n, static_cast<const double*>(A), lda, static_cast<double*>(B), ldb);
+    else
+        cpu_trsm(lower, trans, unit, m, n, static_cast<const float*>(A), lda, static_cast<float*>(B), ldb);
+}
+
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

@@ -28,6 +28,9 @@ void Combine(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, 
 // global index map (i0 + i*is, j0 + j*js) (ScaleTrapezoid.hpp, AxpyTrapezoid)
 void Trapezoid(Device dev, DType t, bool lower, Int m, Int n, double alpha, const void* X, Int ldx, double beta,
                void* Y, Int ldy, Int i0, Int is, Int j0, Int js, Int offset, hipStream_t s);
+// op(A) X = B in place, A m x m (LocalTrsm / blas::Trsm, Left side); f64/f32
+void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, const void* A, Int lda, void* B,
+          Int ldb, hipStream_t s);
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s);
 // host-side scalar conversion of one element (for Get/Set and tests)

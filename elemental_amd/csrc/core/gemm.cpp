@@ -690,6 +690,65 @@ void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMa
     SummaC(oA, oB, alpha, B, A, 1.0, C, uplo);
 }
 
+// Trsm on DistMatrices (src/blas_like/level3/Trsm.cpp:129-420): B := alpha
+// op(A)^-1 B (LEFT) or alpha B op(A)^-1 (RIGHT).  LEFT follows Trsm/LLN.hpp:40-70
+// (and LUN/LLT/LUT with the block order reversed where op(A) is upper):
+//   A11[*,*] <- A11;  X1[*,VR] <- X1;  X1[*,VR] := op(A11)^-1 X1 (trsm_kernel);
+//   X1 <- X1[*,VR];   X_rest -= op(A)_rest,1 X1 (the C-stationary SUMMA on views:
+//   op(A) panel gathered [MC,*] / [*,MC], X1 as [*,MR], MFMA update).
+// RIGHT solves the transposed LEFT problem (X op(A) = B <=> op(A)^T X^T = B^T)
+// through two distributed transposes.  f64/f32 (the reference's GPU Trsm types).
+void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatrix& XPre) {
+    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
+    const DistMatrix& A = *Ap;
+    RWProxy Xp(XPre);
+    DistMatrix& X = Xp.Get();
+    const Int m = X.Height(), n = X.Width(), nb = std::max<Int>(1, g_blocksize);
+    const bool trans = orient != ELX_NORMAL, lower = uplo == ELX_LOWER;
+    const bool forward = lower != trans;  // op(A) lower: blocks top to bottom
+    const Int nblk = (m + nb - 1) / nb;
+    auto A11s = A.Like(Dist::STAR, Dist::STAR);
+    auto X1v = X.Like(Dist::STAR, Dist::VR);
+    for (Int bi = 0; bi < nblk; ++bi) {
+        const Int b = forward ? bi : nblk - 1 - bi;
+        const Int k0 = b * nb, k1 = std::min(m, k0 + nb);
+        Copy(*DistMatrix::View(A, k0, k1, k0, k1), *A11s);  // A11[*,*] <- A11[MC,MR]
+        auto X1 = DistMatrix::View(X, k0, k1, 0, n);
+        X1v->AlignRows(X.RowAlign(), true);
+        Copy(*X1, *X1v);                                     // X1[*,VR] <- X1[MC,MR]
+        if (X.Dev() == Device::GPU) FenceStreams(A11s->Stream(), X1v->Stream());
+        exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, X1v->LocalWidth(), A11s->Buffer(), A11s->LDim(),
+                   X1v->Buffer(), X1v->LDim(), X1v->Stream());
+        Copy(*X1v, *X1);                                     // X1[MC,MR] <- X1[*,VR]
+        // op(A)(rows, k0:k1) for the rows still to solve
+        const Int r0 = forward ? k1 : 0, r1 = forward ? m : k0;
+        if (r1 > r0 && n > 0) {
+            auto Ar = trans ? DistMatrix::View(A, k0, k1, r0, r1) : DistMatrix::View(A, r0, r1, k0, k1);
+            auto Xr = DistMatrix::View(X, r0, r1, 0, n);
+            SummaC(trans ? ELX_TRANSPOSE : ELX_NORMAL, ELX_NORMAL, -1.0, *Ar, *X1, 1.0, *Xr);
+        }
+    }
+    Xp.Finish();
+}
+
+void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B) {
+    ELX_REQUIRE(side == ELX_LEFT || side == ELX_RIGHT, "Trsm: bad LeftOrRight ", side);
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Trsm: bad UpperOrLower ", uplo);
+    ELX_REQUIRE(orient >= ELX_NORMAL && orient <= ELX_ADJOINT, "Trsm: bad orientation");
+    ELX_REQUIRE(diag == ELX_NON_UNIT || diag == ELX_UNIT, "Trsm: bad UnitOrNonUnit ", diag);
+    ELX_REQUIRE(&A.G() == &B.G(), "Trsm: matrices on different grids");
+    ELX_REQUIRE(A.Type() == B.Type(), "Trsm: mixed types");
+    if (A.Type() != DType::F64 && A.Type() != DType::F32) throw LogicError("Trsm: only float and double are supported");
+    if (A.Height() != A.Width()) throw LogicError("A must be square");  // Trsm.cpp:142-143
+    if ((side == ELX_LEFT ? B.Height() : B.Width()) != A.Height()) throw LogicError("Nonconformal Trsm");
+    Scale(alpha, B);  // Trsm.cpp:155 (B *= alpha)
+    if (side == ELX_LEFT) return TrsmLeft(uplo, orient, diag == ELX_UNIT, A, B);
+    auto Bt = B.Like(Dist::MC, Dist::MR);
+    Transpose(B, *Bt);
+    TrsmLeft(uplo, orient == ELX_NORMAL ? ELX_TRANSPOSE : ELX_NORMAL, diag == ELX_UNIT, A, *Bt);
+    Transpose(*Bt, B);
+}
+
 void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,
           int alg) {
     ELX_REQUIRE(oA >= ELX_NORMAL && oA <= ELX_ADJOINT && oB >= ELX_NORMAL && oB <= ELX_ADJOINT, "bad orientation");

@@ -24,6 +24,8 @@ void Trrk(int uplo, int oA, int oB, double alpha, const DistMatrix& A, const Dis
 // C := alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on C's uplo triangle (Syr2k.cpp:78-93)
 void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
            DistMatrix& C);
+// B := alpha op(A)^-1 B (LEFT) / alpha B op(A)^-1 (RIGHT)  (Trsm.cpp:129-420)
+void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B);
 
 void SetBlocksize(Int nb);
 Int Blocksize();

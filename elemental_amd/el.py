@@ -17,13 +17,13 @@ from . import _lib as L
 from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_CANNON, GEMM_DEFAULT,
                    GEMM_SUMMA_A, GEMM_SUMMA_A_MS, GEMM_SUMMA_B, GEMM_SUMMA_B_MS, GEMM_SUMMA_C,
                    GEMM_SUMMA_C_MS, GEMM_SUMMA_DOT, GPU, MC, MD, MR, NORMAL, ROW_MAJOR, STAR, TRANSPOSE,
-                   FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT, LOWER, UPPER,
+                   FILE_AUTO, FILE_BINARY, FILE_BINARY_FLAT, LOWER, UPPER, LEFT, RIGHT, NON_UNIT, UNIT,
                    VC, VR, call, lib)
 
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
-    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "ScaleTrapezoid", "LOWER", "UPPER",
+    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -288,6 +288,12 @@ def Syr2k(uplo, orientation, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistM
 def Her2k(uplo, orientation, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix):
     """El::Her2k: Syr2k with conjugation, identical for the real types."""
     Syr2k(uplo, orientation, alpha, A, B, beta, C, conjugate=True)
+
+
+def Trsm(side, uplo, orientation, diag, alpha, A: DistMatrix, B: DistMatrix):
+    """El::Trsm(side, uplo, orientation, diag, alpha, A, B) (Trsm.cpp:129-420): B is
+    overwritten with alpha op(A)^-1 B (LEFT) or alpha B op(A)^-1 (RIGHT)."""
+    call("elx_trsm", side, uplo, orientation, diag, float(alpha), A.h, B.h)
 
 
 def ScaleTrapezoid(alpha, uplo, A: DistMatrix, offset: int = 0):

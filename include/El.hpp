@@ -28,6 +28,8 @@ enum Dist { MC = ELX_MC, MD = ELX_MD, MR = ELX_MR, VC = ELX_VC, VR = ELX_VR, STA
 enum DistWrap { ELEMENT = 0, BLOCK = 1 };
 enum Orientation { NORMAL = ELX_NORMAL, TRANSPOSE = ELX_TRANSPOSE, ADJOINT = ELX_ADJOINT };
 enum UpperOrLower { LOWER = ELX_LOWER, UPPER = ELX_UPPER };
+enum LeftOrRight { LEFT = ELX_LEFT, RIGHT = ELX_RIGHT };
+enum UnitOrNonUnit { NON_UNIT = ELX_NON_UNIT, UNIT = ELX_UNIT };
 enum GridOrder { ROW_MAJOR = ELX_ROW_MAJOR, COLUMN_MAJOR = ELX_COLUMN_MAJOR };
 enum GemmAlgorithm {
     GEMM_DEFAULT = ELX_GEMM_DEFAULT, GEMM_SUMMA_A_MS = ELX_GEMM_SUMMA_A_MS, GEMM_SUMMA_A = ELX_GEMM_SUMMA_A,
@@ -291,6 +293,11 @@ template <typename T>
 void Her2k(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDistMatrix<T>& A,
            const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
     Syr2k(uplo, orientation, alpha, A, B, beta, C, true);
+}
+template <typename T>
+void Trsm(LeftOrRight side, UpperOrLower uplo, Orientation orientation, UnitOrNonUnit diag, T alpha,
+          const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) {
+    detail::Check(elx_trsm(side, uplo, orientation, diag, detail::ToDouble(alpha), A.h(), B.h()));
 }
 template <typename T>
 void ScaleTrapezoid(T alpha, UpperOrLower uplo, AbstractDistMatrix<T>& A, Int offset = 0) {

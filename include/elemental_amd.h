@@ -55,6 +55,11 @@ extern "C" {
 /* El::UpperOrLower  include/El/core/types.hpp:511-515 */
 #define ELX_LOWER 0
 #define ELX_UPPER 1
+/* El::LeftOrRight / El::UnitOrNonUnit  include/El/core/types.hpp:418-422,489-493 */
+#define ELX_LEFT     0
+#define ELX_RIGHT    1
+#define ELX_NON_UNIT 0
+#define ELX_UNIT     1
 /* El::GridOrder  include/El/core/types.hpp:408-413 */
 #define ELX_ROW_MAJOR    0
 #define ELX_COLUMN_MAJOR 1
@@ -308,6 +313,9 @@ int elx_trrk(int uplo, int orientA, int orientB, double alpha, elx_dm_t A, elx_d
  * C := alpha (op(A) op(B)^T + op(B) op(A)^T) + beta C on C's uplo triangle */
 int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double beta,
               elx_dm_t C, int conjugate);
+/* El::Trsm on DistMatrices (src/blas_like/level3/Trsm.cpp:129-420): B := alpha
+ * op(A)^-1 B (ELX_LEFT) or alpha B op(A)^-1 (ELX_RIGHT); float and double */
+int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B);
 /* A := alpha A on its uplo trapezoid (include/El/blas_like/level1/ScaleTrapezoid.hpp:47-88) */
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset);
 /* Blocksize stack (src/core/environment.cpp:315: default 128) */

@@ -229,6 +229,30 @@ def syr2k(uplo: str, trans: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: n
     return out
 
 
+def trsm(side: str, uplo: str, trans: str, diag: str, alpha, A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """BLAS xTRSM semantics (the reference's CPU path: Trsm.cpp -> blas::Trsm;
+    distributed Trsm.cpp:129-420): X = alpha op(A)^-1 B (side 'L') or
+    alpha B op(A)^-1 ('R'); only A's uplo triangle is read, its diagonal only when
+    diag == 'N'.  Column-oriented substitution in float64."""
+    A = np.asarray(A, dtype=np.float64)
+    X = alpha * np.array(B, dtype=np.float64)
+    m = A.shape[0]
+    i, j = np.indices((m, m))
+    T = np.where((i >= j) if uplo == "L" else (i <= j), A, 0.0)  # the other triangle is never read
+    if diag == "U":
+        np.fill_diagonal(T, 1.0)
+    op = T.T if trans != "N" else T
+    if side == "R":  # X op(A) = B  <=>  op(A)^T X^T = B^T
+        op, X = op.T, X.T
+    lower = bool(np.allclose(op, np.tril(op)))
+    order = range(m) if lower else range(m - 1, -1, -1)
+    for i in order:
+        X[i] /= op[i, i]
+        rest = slice(i + 1, m) if lower else slice(0, i)
+        X[rest] -= np.outer(op[rest, i], X[i])
+    return X.T.copy() if side == "R" else X
+
+
 def cpu_gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """bench.py's CPU baseline: blocked OpenMP f64 GEMM (cpu_gemm.c), BLAS semantics."""
     C = np.array(C, order="F", copy=True, dtype=np.float64)

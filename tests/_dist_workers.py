@@ -214,6 +214,49 @@ def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         raise
 
 
+def trsm_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, m: int, n: int, nb: int,
+                seed: int):
+    """El::Trsm, every side x uplo x orientation x diag (Trsm/{LLN,...,RUT}.hpp),
+    against oracle.trsm; the triangle (and unit diagonal) A must not read is NaN."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = np.float64 if dtype == el.F64 else np.float32
+        el.SetBlocksize(nb)
+        for side in (el.LEFT, el.RIGHT):
+            for uplo in (el.LOWER, el.UPPER):
+                for orient in (el.NORMAL, el.TRANSPOSE):
+                    for diag in (el.NON_UNIT, el.UNIT):
+                        k = m if side == el.LEFT else n
+                        Ag = oracle.hash_matrix(k, k, seed + 1, 0.0, 0.3, npdt)
+                        Ag[np.diag_indices(k)] += npdt(2.0)
+                        i, j = np.indices((k, k))
+                        Ag[(i < j) if uplo == el.LOWER else (i > j)] = np.nan
+                        if diag == el.UNIT:
+                            Ag[np.diag_indices(k)] = np.nan
+                        Bg = oracle.hash_matrix(m, n, seed + 2, -1.0, 1.0, npdt)
+                        alpha = 0.75
+                        ref = oracle.trsm("LR"[side], "LU"[uplo], ORIENTS[orient], "NU"[diag], alpha, Ag, Bg)
+                        A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=k, width=k)
+                        B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
+                        A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+                        B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
+                        el.Trsm(side, uplo, orient, diag, alpha, A, B)
+                        got = B.get_local().astype(np.float64)
+                        want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank)
+                        num = np.linalg.norm(got - want) if got.size else 0.0
+                        den = np.linalg.norm(ref) * k * _tol(dtype)
+                        assert np.isfinite(got).all() and num <= 10 * den, \
+                            (f"Trsm side {side} uplo {uplo} orient {orient} diag {diag} {m}x{n} nb {nb} "
+                             f"grid {r}x{c} rank {rank}: {num / den:.3g}")
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 def cannon_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, seed: int):
     """Cannon_NN (src/blas_like/level3/Gemm/NN.hpp:21-104) on a square grid with
     misaligned A, B and C (exercises the initial skew shifts), against the

@@ -55,6 +55,12 @@ def test_syrk_herk(world, height, cols, monkeypatch):
     _spawn(W.syrk_worker, world, height, el.CPU, el.F64, [(23, 9), (7, 30)], 4, 17)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1), (2, 2), (4, 2)])
+def test_trsm(world, height):
+    """El::Trsm LEFT/RIGHT x LOWER/UPPER x N/T x NON_UNIT/UNIT, ragged blocks (nb = 4)."""
+    _spawn(W.trsm_worker, world, height, el.CPU, el.F64, 19, 13, 4, 31)
+
+
 @pytest.mark.parametrize("world,height", [(1, 1), (4, 2), (2, 1)])
 def test_gemm_cannon(world, height):
     """Cannon_NN on 1x1 and 2x2 with random alignments; LogicError on a 2x1 grid,

@@ -225,3 +225,34 @@ def test_gpu_syrk_large(dtype):
             num = np.linalg.norm((got.astype(np.float64) - ref)[inside])
             den = np.linalg.norm(Ag) ** 2 * k * eps
             assert num <= 10 * den, (uplo, orient, num / den)
+
+
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1), (4, 2)])
+def test_gpu_trsm_distributed(world, height):
+    """El::Trsm, all 16 side/uplo/orientation/diag cases, on the GPU (trsm_kernel +
+    the SUMMA trailing update), host-staged ranks on one device."""
+    _spawn(W.trsm_worker, world, height, el.GPU, el.F64, 45, 23, 16, 41)
+
+
+@pytest.mark.parametrize("dtype", [el.F64, el.F32])
+def test_gpu_trsm_large(dtype):
+    """1x1 grid, m = 1500 (12 blocks of 128, a ragged last one), 700 right-hand
+    sides: LEFT LOWER and UPPER, NORMAL and TRANSPOSE, against oracle.trsm."""
+    m, n = 1500, 700
+    npdt = np.float64 if dtype == el.F64 else np.float32
+    g = el.Grid()
+    el.SetBlocksize(128)
+    Ag = oracle.hash_matrix(m, m, 51, 0.0, 0.05, npdt)
+    Ag[np.diag_indices(m)] += npdt(2.0)
+    Bg = oracle.hash_matrix(m, n, 52, -1.0, 1.0, npdt)
+    for uplo in (el.LOWER, el.UPPER):
+        for orient in (el.NORMAL, el.TRANSPOSE):
+            A = el.DistMatrix(g, dtype, height=m, width=m)
+            B = el.DistMatrix(g, dtype, height=m, width=n)
+            A.set_local(Ag)
+            B.set_local(Bg)
+            el.Trsm(el.LEFT, uplo, orient, el.NON_UNIT, 1.0, A, B)
+            got = B.get_local().astype(np.float64)
+            ref = oracle.trsm("L", "LU"[uplo], "NT"[orient], "N", 1.0, Ag, Bg)
+            err = np.linalg.norm(got - ref) / (np.linalg.norm(ref) * m * np.finfo(npdt).eps)
+            assert err <= 10, (uplo, orient, err)
