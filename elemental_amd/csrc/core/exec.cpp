@@ -296,7 +296,20 @@ void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, 
     if (t != DType::F64 && t != DType::F32) throw LogicError("Trsm: only float and double are supported");
     if (m <= 0 || n <= 0) return;
     if (dev == Device::GPU) {
-        check(kern::trsm_local((int)t, lower, trans, unit, m, n, A, lda, B, ldb, s), "trsm_local");
+        const size_t es = DTypeSize(t);
+        if (m <= 256 && n >= 4 * m) {
+            // many right-hand sides: W = op(A)^-1 (m lanes of substitution), then
+            // B := W B as one MFMA GEMM through a workspace (the inverted-diagonal-
+            // block scheme of vendor trsm), instead of n/64 waves each running an
+            // m^2/2-long dependent chain
+            Buffer W(dev, (size_t)m * m * es, s), T(dev, (size_t)m * n * es, s);
+            check(kern::trsm_local((int)t, true, lower, trans, unit, m, m, A, lda, W.data(), m, s), "trsm_local");
+            Gemm(dev, t, false, false, m, n, m, 1.0, W.data(), m, B, ldb, 0.0, T.data(), m, s);
+            const Copy2D d{m, n, T.data(), 1, m, B, 1, ldb};
+            Copy2DBatch(dev, t, &d, 1, false, 0.0, s);
+            return;
+        }
+        check(kern::trsm_local((int)t, false, lower, trans, unit, m, n, A, lda, B, ldb, s), "trsm_local");
         return;
     }
     if (t == DType::F64)

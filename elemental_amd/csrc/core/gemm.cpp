@@ -698,6 +698,14 @@ void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMa
 //   op(A) panel gathered [MC,*] / [*,MC], X1 as [*,MR], MFMA update).
 // RIGHT solves the transposed LEFT problem (X op(A) = B <=> op(A)^T X^T = B^T)
 // through two distributed transposes.  f64/f32 (the reference's GPU Trsm types).
+Int TrsmOuter() {  // ELX_TRSM_OUTER overrides (tests: several outer blocks at small sizes)
+    static const Int v = [] {
+        const char* e = getenv("ELX_TRSM_OUTER");
+        return e && atoll(e) > 0 ? (Int)atoll(e) : Int(1024);
+    }();
+    return v;
+}
+
 void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatrix& XPre) {
     auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
     const DistMatrix& A = *Ap;
@@ -706,27 +714,42 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     const Int m = X.Height(), n = X.Width(), nb = std::max<Int>(1, g_blocksize);
     const bool trans = orient != ELX_NORMAL, lower = uplo == ELX_LOWER;
     const bool forward = lower != trans;  // op(A) lower: blocks top to bottom
-    const Int nblk = (m + nb - 1) / nb;
     auto A11s = A.Like(Dist::STAR, Dist::STAR);
     auto X1v = X.Like(Dist::STAR, Dist::VR);
-    for (Int bi = 0; bi < nblk; ++bi) {
-        const Int b = forward ? bi : nblk - 1 - bi;
-        const Int k0 = b * nb, k1 = std::min(m, k0 + nb);
-        Copy(*DistMatrix::View(A, k0, k1, k0, k1), *A11s);  // A11[*,*] <- A11[MC,MR]
-        auto X1 = DistMatrix::View(X, k0, k1, 0, n);
-        X1v->AlignRows(X.RowAlign(), true);
-        Copy(*X1, *X1v);                                     // X1[*,VR] <- X1[MC,MR]
-        if (X.Dev() == Device::GPU) FenceStreams(A11s->Stream(), X1v->Stream());
-        exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, X1v->LocalWidth(), A11s->Buffer(), A11s->LDim(),
-                   X1v->Buffer(), X1v->LDim(), X1v->Stream());
-        Copy(*X1v, *X1);                                     // X1[MC,MR] <- X1[*,VR]
-        // op(A)(rows, k0:k1) for the rows still to solve
-        const Int r0 = forward ? k1 : 0, r1 = forward ? m : k0;
-        if (r1 > r0 && n > 0) {
-            auto Ar = trans ? DistMatrix::View(A, k0, k1, r0, r1) : DistMatrix::View(A, r0, r1, k0, k1);
-            auto Xr = DistMatrix::View(X, r0, r1, 0, n);
-            SummaC(trans ? ELX_TRANSPOSE : ELX_NORMAL, ELX_NORMAL, -1.0, *Ar, *X1, 1.0, *Xr);
+    // X_rest -= op(A)(r0:r1, k0:k1) X(k0:k1, :) through the SUMMA pipeline on views
+    auto update = [&](Int r0, Int r1, Int k0, Int k1) {
+        if (r1 <= r0 || n == 0) return;
+        auto Ar = trans ? DistMatrix::View(A, k0, k1, r0, r1) : DistMatrix::View(A, r0, r1, k0, k1);
+        auto Xk = DistMatrix::View(X, k0, k1, 0, n);
+        auto Xr = DistMatrix::View(X, r0, r1, 0, n);
+        SummaC(trans ? ELX_TRANSPOSE : ELX_NORMAL, ELX_NORMAL, -1.0, *Ar, *Xk, 1.0, *Xr);
+    };
+    // Two levels: outer blocks of TrsmOuter() (1024) rows (whole nb blocks) carry the
+    // trailing update as one deep (k = outer) MFMA GEMM; inside an outer block
+    // the reference's nb-step runs (Trsm/LLN.hpp:40-70) with updates confined to
+    // it.  Same eliminations, fewer and deeper launches than k = nb updates.
+    const Int ob = std::max<Int>(nb, (TrsmOuter() + nb - 1) / nb * nb);
+    const Int nouter = (m + ob - 1) / ob;
+    for (Int oi = 0; oi < nouter; ++oi) {
+        const Int o = forward ? oi : nouter - 1 - oi;
+        const Int K0 = o * ob, K1 = std::min(m, K0 + ob);
+        const Int nblk = (K1 - K0 + nb - 1) / nb;
+        for (Int bi = 0; bi < nblk; ++bi) {
+            const Int b = forward ? bi : nblk - 1 - bi;
+            const Int k0 = K0 + b * nb, k1 = std::min(K1, k0 + nb);
+            Copy(*DistMatrix::View(A, k0, k1, k0, k1), *A11s);  // A11[*,*] <- A11[MC,MR]
+            auto X1 = DistMatrix::View(X, k0, k1, 0, n);
+            X1v->AlignRows(X.RowAlign(), true);
+            Copy(*X1, *X1v);                                     // X1[*,VR] <- X1[MC,MR]
+            if (X.Dev() == Device::GPU) FenceStreams(A11s->Stream(), X1v->Stream());
+            exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, X1v->LocalWidth(), A11s->Buffer(),
+                       A11s->LDim(), X1v->Buffer(), X1v->LDim(), X1v->Stream());
+            Copy(*X1v, *X1);                                     // X1[MC,MR] <- X1[*,VR]
+            if (forward) update(k1, K1, k0, k1);
+            else update(K0, k0, k0, k1);
         }
+        if (forward) update(K1, m, K0, K1);
+        else update(0, K0, K0, K1);
     }
     Xp.Finish();
 }

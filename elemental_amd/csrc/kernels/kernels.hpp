@@ -86,8 +86,9 @@ hipError_t fill_hash(int dtype, i64 m, i64 n, void* A, i64 lda, i64 i0, i64 istr
 // lies in the lower (gi >= gj - offset) or upper (gi <= gj - offset) trapezoid.
 hipError_t trapezoid2d(int dtype, bool lower, i64 m, i64 n, double alpha, const void* X, i64 ldx, double beta,
                        void* Y, i64 ldy, i64 i0, i64 istride, i64 j0, i64 jstride, i64 offset, hipStream_t s);
-// op(A) X = B in place (A m x m, uplo triangle, unit diagonal optional); f64/f32 only
-hipError_t trsm_local(int dtype, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda, void* B,
-                      i64 ldb, hipStream_t s);
+// op(A) X = B in place (A m x m, uplo triangle, unit diagonal optional); f64/f32 only.
+// ident: B (m x m) is output only and becomes op(A)^-1.
+hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda,
+                      void* B, i64 ldb, hipStream_t s);
 }  // namespace kern
 }  // namespace elx

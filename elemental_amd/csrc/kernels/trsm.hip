@@ -9,8 +9,9 @@
 // loads that hit the L1/L2), then written back.  Column-oriented substitution:
 // x_i /= a_ii, then x_r -= a_ri x_i for the rows r still to come.  m is the
 // distributed block size (<= MAXM rows per LDS pass; larger m falls back to the
-// same loop on global memory).  The solve is O(m^2 n) against the O(m n K)
-// trailing GEMM, so it is a small share of the Trsm time at the configs' sizes.
+// same loop on global memory).  The substitution is a dependent chain per lane,
+// so with many right-hand sides exec::Trsm instead inverts the block (IDENT: the
+// identity as right-hand sides, m lanes) and applies op(A)^-1 as one MFMA GEMM.
 #include "kernels.hpp"
 #include "../common.hpp"
 
@@ -20,7 +21,8 @@ namespace {
 
 constexpr int WAVE = 64;
 
-template <typename T, bool LDS>
+// IDENT: the right-hand sides are the identity (B is output only): B := op(A)^-1
+template <typename T, bool LDS, bool IDENT>
 __global__ __launch_bounds__(WAVE) void trsm_kernel(bool lower, bool trans, bool unit, i64 m, i64 n, const T* A,
                                                     i64 lda, T* B, i64 ldb) {
     extern __shared__ unsigned char smem[];
@@ -30,49 +32,68 @@ __global__ __launch_bounds__(WAVE) void trsm_kernel(bool lower, bool trans, bool
     T* bcol = B + (live ? col : 0) * ldb;
     // element (r) of this lane's right-hand side
     auto X = [&](i64 r) -> T& { return LDS ? x[r * WAVE + threadIdx.x] : bcol[r]; };
-    if (LDS && live)
-        for (i64 r = 0; r < m; ++r) x[r * WAVE + threadIdx.x] = bcol[r];
+    if (live) {
+        if (IDENT)
+            for (i64 r = 0; r < m; ++r) X(r) = r == col ? T(1) : T(0);
+        else if (LDS)
+            for (i64 r = 0; r < m; ++r) x[r * WAVE + threadIdx.x] = bcol[r];
+    }
     auto opA = [&](i64 r, i64 c) { return trans ? A[c + r * lda] : A[r + c * lda]; };
     const bool forward = lower != trans;  // op(A) lower triangular
-    if (live) {
-        for (i64 s = 0; s < m; ++s) {
-            const i64 i = forward ? s : m - 1 - s;
-            T xi = X(i);
-            if (!unit) xi = xi / opA(i, i);
-            X(i) = xi;
-            if (forward)
-                for (i64 r = i + 1; r < m; ++r) X(r) = X(r) - opA(r, i) * xi;
-            else
-                for (i64 r = 0; r < i; ++r) X(r) = X(r) - opA(r, i) * xi;
+    // LDS mode: column i of op(A) is staged into LDS by the whole wave before
+    // the step (independent loads, one latency per step instead of one per row)
+    T* acol = x + m * WAVE;
+    for (i64 s = 0; s < m; ++s) {
+        const i64 i = forward ? s : m - 1 - s;
+        const i64 lo = forward ? i : 0, hi = forward ? m : i + 1;  // rows touched by step i
+        if (LDS) {
+            __syncthreads();
+            for (i64 r = lo + threadIdx.x; r < hi; r += WAVE) acol[r] = opA(r, i);
+            __syncthreads();
         }
+        if (!live) continue;
+        T xi = X(i);
+        if (!unit) xi = xi / (LDS ? acol[i] : opA(i, i));
+        X(i) = xi;
+        if (forward)
+            for (i64 r = i + 1; r < m; ++r) X(r) = X(r) - (LDS ? acol[r] : opA(r, i)) * xi;
+        else
+            for (i64 r = 0; r < i; ++r) X(r) = X(r) - (LDS ? acol[r] : opA(r, i)) * xi;
     }
     if (LDS && live)
         for (i64 r = 0; r < m; ++r) bcol[r] = x[r * WAVE + threadIdx.x];
 }
 
 template <typename T>
-hipError_t launch_trsm(bool lower, bool trans, bool unit, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb,
-                       hipStream_t s) {
+hipError_t launch_trsm(bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const T* A, i64 lda, T* B,
+                       i64 ldb, hipStream_t s) {
     const dim3 grid((unsigned)((n + WAVE - 1) / WAVE));
-    const size_t lds = (size_t)m * WAVE * sizeof(T);
-    if (lds <= 64 * 1024)
-        hipLaunchKernelGGL((trsm_kernel<T, true>), grid, dim3(WAVE), lds, s, lower, trans, unit, m, n, A, lda, B, ldb);
-    else
-        hipLaunchKernelGGL((trsm_kernel<T, false>), grid, dim3(WAVE), 0, s, lower, trans, unit, m, n, A, lda, B, ldb);
+    const size_t lds = (size_t)m * (WAVE + 1) * sizeof(T);
+    if (lds <= 66 * 1024) {
+        if (ident)
+            hipLaunchKernelGGL((trsm_kernel<T, true, true>), grid, dim3(WAVE), lds, s, lower, trans, unit, m, n, A, lda, B, ldb);
+        else
+            hipLaunchKernelGGL((trsm_kernel<T, true, false>), grid, dim3(WAVE), lds, s, lower, trans, unit, m, n, A, lda, B, ldb);
+    } else {
+        if (ident)
+            hipLaunchKernelGGL((trsm_kernel<T, false, true>), grid, dim3(WAVE), 0, s, lower, trans, unit, m, n, A, lda, B, ldb);
+        else
+            hipLaunchKernelGGL((trsm_kernel<T, false, false>), grid, dim3(WAVE), 0, s, lower, trans, unit, m, n, A, lda, B, ldb);
+    }
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t trsm_local(int dtype, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda, void* B,
-                      i64 ldb, hipStream_t s) {
+hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda,
+                      void* B, i64 ldb, hipStream_t s) {
     if (m <= 0 || n <= 0) return hipSuccess;
     if (n > (i64)WAVE * 0x7fffffff) return hipErrorInvalidValue;
     switch (dtype) {
     case ELX_F64:
-        return launch_trsm(lower, trans, unit, m, n, static_cast<const double*>(A), lda, static_cast<double*>(B), ldb, s);
+        return launch_trsm(ident, lower, trans, unit, m, n, static_cast<const double*>(A), lda, static_cast<double*>(B), ldb, s);
     case ELX_F32:
-        return launch_trsm(lower, trans, unit, m, n, static_cast<const float*>(A), lda, static_cast<float*>(B), ldb, s);
+        return launch_trsm(ident, lower, trans, unit, m, n, static_cast<const float*>(A), lda, static_cast<float*>(B), ldb, s);
     default:
         return hipErrorInvalidValue;
     }
