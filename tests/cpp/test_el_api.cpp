@@ -90,6 +90,28 @@ int main() {
             err = std::max(err, std::fabs(e[i + j * k] - (i > j ? d[i + j * k] : i == j ? 3.0 * d[i + j * k] : d[i + j * k])));
     EXPECT(err <= 1e-12);
 
+    // Trsm: solve tril(E) Y = 2 R (R: k x n right-hand sides taken from C; E's
+    // diagonal is 3 d_ii > 0 after the Herk above); check tril(E) Y == 2 R
+    {
+        const auto c_now = Local(C);
+        std::vector<double> rhs(k * n);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < k; ++i) rhs[i + j * k] = c_now[(i % m) + j * m];
+        El::DistMatrix<double> Y(k, n, g);
+        Y.SetLocalBlock(rhs.data(), k);
+        El::Trsm(El::LEFT, El::LOWER, El::NORMAL, El::NON_UNIT, 2.0, E, Y);
+        const auto y = Local(Y);
+        double rerr = 0, rref = 0;
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < k; ++i) {
+                double s = 0;
+                for (Int l = 0; l <= i; ++l) s += e[i + l * k] * y[l + j * k];
+                rerr = std::max(rerr, std::fabs(s - 2.0 * rhs[i + j * k]));
+                rref = std::max(rref, std::fabs(rhs[i + j * k]));
+            }
+        EXPECT(rerr <= 1e-10 * (rref + 1));
+    }
+
     // redistribution + transpose + view are bit-exact
     El::DistMatrix<double, El::STAR, El::STAR> S(A);
     EXPECT(Local(S) == a);
