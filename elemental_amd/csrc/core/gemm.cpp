@@ -737,14 +737,26 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
         for (Int bi = 0; bi < nblk; ++bi) {
             const Int b = forward ? bi : nblk - 1 - bi;
             const Int k0 = K0 + b * nb, k1 = std::min(K1, k0 + nb);
-            Copy(*DistMatrix::View(A, k0, k1, k0, k1), *A11s);  // A11[*,*] <- A11[MC,MR]
+            // a block whose local storage already IS the [*,*] / [*,VR] layout (a
+            // 1x1 grid) is used in place: no redistribution temporaries
+            auto A11 = DistMatrix::View(A, k0, k1, k0, k1);
+            std::shared_ptr<const DistMatrix> a11 = A11;
+            if (!SameLocalLayout(*A11, Dist::STAR, Dist::STAR, 0, 0)) {
+                Copy(*A11, *A11s);                               // A11[*,*] <- A11[MC,MR]
+                a11 = A11s;
+            }
             auto X1 = DistMatrix::View(X, k0, k1, 0, n);
-            X1v->AlignRows(X.RowAlign(), true);
-            Copy(*X1, *X1v);                                     // X1[*,VR] <- X1[MC,MR]
-            if (X.Dev() == Device::GPU) FenceStreams(A11s->Stream(), X1v->Stream());
-            exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, X1v->LocalWidth(), A11s->Buffer(),
-                       A11s->LDim(), X1v->Buffer(), X1v->LDim(), X1v->Stream());
-            Copy(*X1v, *X1);                                     // X1[MC,MR] <- X1[*,VR]
+            const bool inplace = SameLocalLayout(*X1, Dist::STAR, Dist::VR, 0, X1->RowAlign());
+            DistMatrix* x1 = X1.get();
+            if (!inplace) {
+                X1v->AlignRows(X.RowAlign(), true);
+                Copy(*X1, *X1v);                                 // X1[*,VR] <- X1[MC,MR]
+                x1 = X1v.get();
+            }
+            if (X.Dev() == Device::GPU) FenceStreams(a11->Stream(), x1->Stream());
+            exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, x1->LocalWidth(), a11->Buffer(), a11->LDim(),
+                       x1->Buffer(), x1->LDim(), x1->Stream());
+            if (!inplace) Copy(*X1v, *X1);                       // X1[MC,MR] <- X1[*,VR]
             if (forward) update(k1, K1, k0, k1);
             else update(K0, k0, k0, k1);
         }
