@@ -302,11 +302,9 @@ void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, 
             // B := W B as one MFMA GEMM through a workspace (the inverted-diagonal-
             // block scheme of vendor trsm), instead of n/64 waves each running an
             // m^2/2-long dependent chain
-            Buffer W(dev, (size_t)m * m * es, s), T(dev, (size_t)m * n * es, s);
+            Buffer W(dev, (size_t)m * m * es, s);
             check(kern::trsm_local((int)t, true, lower, trans, unit, m, m, A, lda, W.data(), m, s), "trsm_local");
-            Gemm(dev, t, false, false, m, n, m, 1.0, W.data(), m, B, ldb, 0.0, T.data(), m, s);
-            const Copy2D d{m, n, T.data(), 1, m, B, 1, ldb};
-            Copy2DBatch(dev, t, &d, 1, false, 0.0, s);
+            ApplyInverse(dev, t, m, n, W.data(), m, B, ldb, s);
             return;
         }
         check(kern::trsm_local((int)t, false, lower, trans, unit, m, n, A, lda, B, ldb, s), "trsm_local");
@@ -316,6 +314,19 @@ void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, 
         cpu_trsm(lower, trans, unit, m, n, static_cast<const double*>(A), lda, static_cast<double*>(B), ldb);
     else
         cpu_trsm(lower, trans, unit, m, n, static_cast<const float*>(A), lda, static_cast<float*>(B), ldb);
+}
+
+void TriInverseBatched(DType t, bool lower, bool trans, bool unit, Int nb, Int m, const void* A, Int lda, void* W,
+                       hipStream_t s) {
+    check(kern::tri_inverse_batched((int)t, lower, trans, unit, nb, m, A, lda, W, s), "tri_inverse_batched");
+}
+
+void ApplyInverse(Device dev, DType t, Int m, Int n, const void* W, Int ldw, void* B, Int ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    Buffer T(dev, (size_t)m * n * DTypeSize(t), s);
+    Gemm(dev, t, false, false, m, n, m, 1.0, W, ldw, B, ldb, 0.0, T.data(), m, s);
+    const Copy2D d{m, n, T.data(), 1, m, B, 1, ldb};
+    Copy2DBatch(dev, t, &d, 1, false, 0.0, s);
 }
 
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,

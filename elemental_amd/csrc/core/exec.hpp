@@ -31,6 +31,12 @@ void Trapezoid(Device dev, DType t, bool lower, Int m, Int n, double alpha, cons
 // op(A) X = B in place, A m x m (LocalTrsm / blas::Trsm, Left side); f64/f32
 void Trsm(Device dev, DType t, bool lower, bool trans, bool unit, Int m, Int n, const void* A, Int lda, void* B,
           Int ldb, hipStream_t s);
+// GPU only: W_b := op(A_bb)^-1 for every nb x nb diagonal block of the m x m A
+// (W_b at W + b*nb*nb, leading dimension nb), one launch
+void TriInverseBatched(DType t, bool lower, bool trans, bool unit, Int nb, Int m, const void* A, Int lda, void* W,
+                       hipStream_t s);
+// B := W B (W m x m) through a workspace: one MFMA GEMM + one copy
+void ApplyInverse(Device dev, DType t, Int m, Int n, const void* W, Int ldw, void* B, Int ldb, hipStream_t s);
 void FillHash(Device dev, DType t, Int m, Int n, void* A, Int lda, Int i0, Int is, Int j0, Int js,
               uint64_t seed, double center, double radius, hipStream_t s);
 // host-side scalar conversion of one element (for Get/Set and tests)

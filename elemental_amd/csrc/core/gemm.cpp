@@ -728,6 +728,20 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     // trailing update as one deep (k = outer) MFMA GEMM; inside an outer block
     // the reference's nb-step runs (Trsm/LLN.hpp:40-70) with updates confined to
     // it.  Same eliminations, fewer and deeper launches than k = nb updates.
+    // A whose local block is the whole matrix (1x1 grid): every diagonal block's
+    // inverse comes from ONE batched launch up front (the per-block inversions
+    // are independent), applied per block as an MFMA GEMM; elsewhere each block
+    // is solved where it lands (exec::Trsm)
+    const size_t es = DTypeSize(X.Type());
+    Buffer winv;
+    const bool batched = X.Dev() == Device::GPU && SameLocalLayout(A, Dist::STAR, Dist::STAR, 0, 0) &&
+                         nb * 65 * (Int)es <= 66 * 1024 && (m + nb - 1) / nb <= 65535 &&
+                         SameLocalLayout(X, Dist::STAR, Dist::VR, 0, X.RowAlign()) && X.LocalWidth() >= 4 * nb;
+    if (batched) {
+        FenceStreams(A.Stream(), X.Stream());
+        winv.Reset(Device::GPU, static_cast<size_t>((m + nb - 1) / nb) * nb * nb * es, X.Stream());
+        exec::TriInverseBatched(X.Type(), lower, trans, unit, nb, m, A.Buffer(), A.LDim(), winv.data(), X.Stream());
+    }
     const Int ob = std::max<Int>(nb, (TrsmOuter() + nb - 1) / nb * nb);
     const Int nouter = (m + ob - 1) / ob;
     for (Int oi = 0; oi < nouter; ++oi) {
@@ -737,6 +751,15 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
         for (Int bi = 0; bi < nblk; ++bi) {
             const Int b = forward ? bi : nblk - 1 - bi;
             const Int k0 = K0 + b * nb, k1 = std::min(K1, k0 + nb);
+            if (batched) {
+                auto X1 = DistMatrix::View(X, k0, k1, 0, n);
+                exec::ApplyInverse(X.Dev(), X.Type(), k1 - k0, X1->LocalWidth(),
+                                   static_cast<const char*>(winv.data()) + (k0 / nb) * nb * nb * es, nb, X1->Buffer(),
+                                   X1->LDim(), X1->Stream());
+                if (forward) update(k1, K1, k0, k1);
+                else update(K0, k0, k0, k1);
+                continue;
+            }
             // a block whose local storage already IS the [*,*] / [*,VR] layout (a
             // 1x1 grid) is used in place: no redistribution temporaries
             auto A11 = DistMatrix::View(A, k0, k1, k0, k1);

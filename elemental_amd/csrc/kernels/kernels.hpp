@@ -90,5 +90,9 @@ hipError_t trapezoid2d(int dtype, bool lower, i64 m, i64 n, double alpha, const 
 // ident: B (m x m) is output only and becomes op(A)^-1.
 hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda,
                       void* B, i64 ldb, hipStream_t s);
+// W_b := op(A_bb)^-1 for every nb x nb diagonal block of A (m x m; the last may be
+// ragged), W_b at W + b*nb*nb with leading dimension nb; one launch.  nb*65*es <= 66 KiB.
+hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64 nb, i64 m, const void* A, i64 lda,
+                               void* W, hipStream_t s);
 }  // namespace kern
 }  // namespace elx

@@ -23,8 +23,8 @@ constexpr int WAVE = 64;
 
 // IDENT: the right-hand sides are the identity (B is output only): B := op(A)^-1
 template <typename T, bool LDS, bool IDENT>
-__global__ __launch_bounds__(WAVE) void trsm_kernel(bool lower, bool trans, bool unit, i64 m, i64 n, const T* A,
-                                                    i64 lda, T* B, i64 ldb) {
+__device__ __forceinline__ void trsm_body(bool lower, bool trans, bool unit, i64 m, i64 n, const T* A, i64 lda, T* B,
+                                          i64 ldb) {
     extern __shared__ unsigned char smem[];
     T* x = reinterpret_cast<T*>(smem);
     const i64 col = (i64)blockIdx.x * WAVE + threadIdx.x;
@@ -64,6 +64,22 @@ __global__ __launch_bounds__(WAVE) void trsm_kernel(bool lower, bool trans, bool
         for (i64 r = 0; r < m; ++r) bcol[r] = x[r * WAVE + threadIdx.x];
 }
 
+template <typename T, bool LDS, bool IDENT>
+__global__ __launch_bounds__(WAVE) void trsm_kernel(bool lower, bool trans, bool unit, i64 m, i64 n, const T* A,
+                                                    i64 lda, T* B, i64 ldb) {
+    trsm_body<T, LDS, IDENT>(lower, trans, unit, m, n, A, lda, B, ldb);
+}
+
+// Every diagonal block of A at once: blockIdx.y = block b (rows/cols [b*nb,
+// min(m, (b+1)*nb))), W_b = op(A_bb)^-1 at W + b*nb*nb with leading dimension nb.
+template <typename T>
+__global__ __launch_bounds__(WAVE) void tri_inverse_batched_kernel(bool lower, bool trans, bool unit, i64 nb, i64 m,
+                                                                   const T* A, i64 lda, T* W) {
+    const i64 b = blockIdx.y, r0 = b * nb;
+    const i64 sz = (m - r0) < nb ? (m - r0) : nb;
+    trsm_body<T, true, true>(lower, trans, unit, sz, sz, A + r0 + r0 * lda, lda, W + b * nb * nb, nb);
+}
+
 template <typename T>
 hipError_t launch_trsm(bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const T* A, i64 lda, T* B,
                        i64 ldb, hipStream_t s) {
@@ -84,6 +100,29 @@ hipError_t launch_trsm(bool ident, bool lower, bool trans, bool unit, i64 m, i64
 }
 
 }  // namespace
+
+hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64 nb, i64 m, const void* A, i64 lda,
+                               void* W, hipStream_t s) {
+    if (m <= 0 || nb <= 0) return hipSuccess;
+    const i64 nblk = (m + nb - 1) / nb;
+    const int es = dtype == ELX_F64 ? 8 : 4;
+    const size_t lds = (size_t)nb * (WAVE + 1) * es;
+    if (lds > 66 * 1024 || nblk > 65535) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((nb + WAVE - 1) / WAVE), (unsigned)nblk);
+    switch (dtype) {
+    case ELX_F64:
+        hipLaunchKernelGGL((tri_inverse_batched_kernel<double>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
+                           static_cast<const double*>(A), lda, static_cast<double*>(W));
+        break;
+    case ELX_F32:
+        hipLaunchKernelGGL((tri_inverse_batched_kernel<float>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
+                           static_cast<const float*>(A), lda, static_cast<float*>(W));
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda,
                       void* B, i64 ldb, hipStream_t s) {
