@@ -119,6 +119,7 @@ _SIGS = {
     "elx_trrk": (_i, [_i, _i, _i, _d, _vp, _vp, _d, _vp]),
     "elx_syr2k": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_trsm": (_i, [_i, _i, _i, _i, _d, _vp, _vp]),
+    "elx_symm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
     "elx_blocksize": (_i64, []),

@@ -349,6 +349,10 @@ int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A,
         Trsm(side, uplo, orient, diag, alpha, M(A), M(B));
     });
 }
+int elx_symm(int side, int uplo, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C, int conjugate) {
+    (void)conjugate;  // real types: Hemm == Symm
+    return Guard([&] { Symm(side, uplo, alpha, M(A), M(B), beta, M(C)); });
+}
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset) {
     return Guard([&] { ScaleTrapezoid(alpha, uplo, M(A), offset); });
 }

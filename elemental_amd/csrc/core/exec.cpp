@@ -265,7 +265,7 @@ void Trapezoid(Device dev, DType t, bool lower, Int m, Int n, double alpha, cons
             for (Int i = 0; i < m; ++i) {
                 const Int gi = i0 + i * is, gj = j0 + j * js - offset;
                 if (lower ? gi < gj : gi > gj) continue;
-                Cm v = (Cm)beta * H<S>::ld(y + i + j * ldy);
+                Cm v = (x && beta == 0.0) ? Cm(0) : (Cm)beta * H<S>::ld(y + i + j * ldy);
                 if (x) v = v + (Cm)alpha * H<S>::ld(x + i + j * ldx);
                 H<S>::st(y + i + j * ldy, v);
             }

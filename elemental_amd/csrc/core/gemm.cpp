@@ -807,6 +807,36 @@ void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatr
     Transpose(*Bt, B);
 }
 
+// Symm / Hemm on DistMatrices (src/blas_like/level3/Symm.cpp:55-80): C := alpha
+// A B + beta C (LEFT) or alpha B A + beta C (RIGHT), A symmetric with only its
+// uplo triangle read.  The reference accumulates triangle-aware local products
+// (Symm/LL.hpp LocalAccumulateLL); here A is completed once into a full [MC,MR]
+// copy (one distributed transpose + a trapezoid copy of the mirrored strict
+// triangle, O(n^2) HBM work) and the product runs through El::Gemm's pipeline.
+void Symm(int side, int uplo, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C) {
+    ELX_REQUIRE(side == ELX_LEFT || side == ELX_RIGHT, "Symm: bad LeftOrRight ", side);
+    ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Symm: bad UpperOrLower ", uplo);
+    ELX_REQUIRE(&A.G() == &B.G() && &A.G() == &C.G(), "Symm: matrices on different grids");
+    ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "Symm: mixed types");
+    if (A.Height() != A.Width()) throw LogicError("A must be square");
+    const bool left = side == ELX_LEFT;
+    if ((left ? B.Height() : B.Width()) != A.Height() || C.Height() != B.Height() || C.Width() != B.Width())
+        throw LogicError("Nonconformal Symm");
+    auto S = A.Like(Dist::MC, Dist::MR);
+    Copy(A, *S);
+    auto T = A.Like(Dist::MC, Dist::MR);
+    T->AlignWith(*S, true);
+    Transpose(*S, *T);
+    // S's strictly-other triangle := T's (lower stored: strict upper is gi <= gj - 1)
+    const bool other_lower = uplo == ELX_UPPER;
+    if (S->Dev() == Device::GPU) FenceStreams(T->Stream(), S->Stream());
+    exec::Trapezoid(S->Dev(), S->Type(), other_lower, S->LocalHeight(), S->LocalWidth(), 1.0, T->Buffer(), T->LDim(),
+                    0.0, S->Buffer(), S->LDim(), S->ColShift(), S->ColStride(), S->RowShift(), S->RowStride(),
+                    other_lower ? -1 : 1, S->Stream());
+    if (left) Gemm(ELX_NORMAL, ELX_NORMAL, alpha, *S, B, beta, C, ELX_GEMM_DEFAULT);
+    else Gemm(ELX_NORMAL, ELX_NORMAL, alpha, B, *S, beta, C, ELX_GEMM_DEFAULT);
+}
+
 void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,
           int alg) {
     ELX_REQUIRE(oA >= ELX_NORMAL && oA <= ELX_ADJOINT && oB >= ELX_NORMAL && oB <= ELX_ADJOINT, "bad orientation");

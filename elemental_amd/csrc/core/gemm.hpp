@@ -26,6 +26,8 @@ void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMa
            DistMatrix& C);
 // B := alpha op(A)^-1 B (LEFT) / alpha B op(A)^-1 (RIGHT)  (Trsm.cpp:129-420)
 void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B);
+// C := alpha A B + beta C (LEFT) / alpha B A + beta C (RIGHT), A symmetric (uplo stored)  (Symm.cpp:55-80)
+void Symm(int side, int uplo, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C);
 
 void SetBlocksize(Int nb);
 Int Blocksize();

@@ -438,7 +438,8 @@ __global__ __launch_bounds__(NT) void hash_kernel(i64 m, i64 n, typename Elem<T>
 // diagonal blocks in Trrk/Local.hpp:155-210).  Element (i,j) of the local block
 // is global (i0 + i*istride, j0 + j*jstride); inside the trapezoid
 // (lower: gi >= gj - offset, upper: gi <= gj - offset) it becomes
-// beta*Y + alpha*X (X may be null: beta*Y), outside it is neither read nor written.
+// beta*Y + alpha*X (X may be null: beta*Y; with X and beta == 0, alpha*X without
+// reading Y), outside it is neither read nor written.
 template <typename T>
 __global__ __launch_bounds__(NT) void trapezoid_kernel(bool lower, i64 m, i64 n, double alpha,
                                                        const typename Elem<T>::storage* X, i64 ldx, double beta,
@@ -450,7 +451,8 @@ __global__ __launch_bounds__(NT) void trapezoid_kernel(bool lower, i64 m, i64 n,
     for_each_2d(m, n, [&](i64 i, i64 j) {
         const i64 gi = i0 + i * istride, gj = j0 + j * jstride - offset;
         if (lower ? gi < gj : gi > gj) return;
-        Cm y = b * E::load(Y[i + j * ldy]);
+        // with X and beta == 0, Y is not read (a trapezoid copy: NaNs there do not survive)
+        Cm y = (X && beta == 0.0) ? Cm(0) : b * E::load(Y[i + j * ldy]);
         if (X) y = y + a * E::load(X[i + j * ldx]);
         Y[i + j * ldy] = E::store(y);
     });

@@ -23,7 +23,7 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
-    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
+    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "Symm", "Hemm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -294,6 +294,16 @@ def Trsm(side, uplo, orientation, diag, alpha, A: DistMatrix, B: DistMatrix):
     """El::Trsm(side, uplo, orientation, diag, alpha, A, B) (Trsm.cpp:129-420): B is
     overwritten with alpha op(A)^-1 B (LEFT) or alpha B op(A)^-1 (RIGHT)."""
     call("elx_trsm", side, uplo, orientation, diag, float(alpha), A.h, B.h)
+
+
+def Symm(side, uplo, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix, conjugate: bool = False):
+    """El::Symm(side, uplo, alpha, A, B, beta, C) (Symm.cpp:55-80): A symmetric, uplo stored."""
+    call("elx_symm", side, uplo, float(alpha), A.h, B.h, float(beta), C.h, int(bool(conjugate)))
+
+
+def Hemm(side, uplo, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix):
+    """El::Hemm: Symm with conjugation, identical for the real types."""
+    Symm(side, uplo, alpha, A, B, beta, C, conjugate=True)
 
 
 def ScaleTrapezoid(alpha, uplo, A: DistMatrix, offset: int = 0):

@@ -300,6 +300,16 @@ void Trsm(LeftOrRight side, UpperOrLower uplo, Orientation orientation, UnitOrNo
     detail::Check(elx_trsm(side, uplo, orientation, diag, detail::ToDouble(alpha), A.h(), B.h()));
 }
 template <typename T>
+void Symm(LeftOrRight side, UpperOrLower uplo, T alpha, const AbstractDistMatrix<T>& A, const AbstractDistMatrix<T>& B,
+          T beta, AbstractDistMatrix<T>& C, bool conjugate = false) {
+    detail::Check(elx_symm(side, uplo, detail::ToDouble(alpha), A.h(), B.h(), detail::ToDouble(beta), C.h(), conjugate));
+}
+template <typename T>
+void Hemm(LeftOrRight side, UpperOrLower uplo, T alpha, const AbstractDistMatrix<T>& A, const AbstractDistMatrix<T>& B,
+          T beta, AbstractDistMatrix<T>& C) {
+    Symm(side, uplo, alpha, A, B, beta, C, true);
+}
+template <typename T>
 void ScaleTrapezoid(T alpha, UpperOrLower uplo, AbstractDistMatrix<T>& A, Int offset = 0) {
     detail::Check(elx_dm_scale_trapezoid(detail::ToDouble(alpha), uplo, A.h(), offset));
 }

@@ -316,6 +316,10 @@ int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double
 /* El::Trsm on DistMatrices (src/blas_like/level3/Trsm.cpp:129-420): B := alpha
  * op(A)^-1 B (ELX_LEFT) or alpha B op(A)^-1 (ELX_RIGHT); float and double */
 int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B);
+/* El::Symm / El::Hemm (src/blas_like/level3/Symm.cpp:55-80): C := alpha A B + beta C
+ * (ELX_LEFT) or alpha B A + beta C (ELX_RIGHT); A symmetric, only its uplo triangle read */
+int elx_symm(int side, int uplo, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C,
+             int conjugate);
 /* A := alpha A on its uplo trapezoid (include/El/blas_like/level1/ScaleTrapezoid.hpp:47-88) */
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset);
 /* Blocksize stack (src/core/environment.cpp:315: default 128) */

@@ -253,6 +253,17 @@ def trsm(side: str, uplo: str, trans: str, diag: str, alpha, A: np.ndarray, B: n
     return X.T.copy() if side == "R" else X
 
 
+def symm(side: str, uplo: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
+    """BLAS xSYMM semantics (Symm.cpp:55-80 -> blas::Symm): A symmetric with only
+    its uplo triangle read; the full A is mirrored, then the GEMM loop nest."""
+    m = A.shape[0]
+    i, j = np.indices((m, m))
+    keep = (i >= j) if uplo == "L" else (i <= j)
+    T = np.where(keep, A, 0.0)
+    S = np.where(keep, A, T.T).astype(A.dtype)
+    return gemm("N", "N", alpha, S, B, beta, C) if side == "L" else gemm("N", "N", alpha, B, S, beta, C)
+
+
 def cpu_gemm(ta: str, tb: str, alpha, A: np.ndarray, B: np.ndarray, beta, C: np.ndarray) -> np.ndarray:
     """bench.py's CPU baseline: blocked OpenMP f64 GEMM (cpu_gemm.c), BLAS semantics."""
     C = np.array(C, order="F", copy=True, dtype=np.float64)

@@ -257,6 +257,44 @@ def trsm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         raise
 
 
+def symm_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, m: int, n: int, seed: int):
+    """El::Symm / El::Hemm LEFT/RIGHT x LOWER/UPPER (Symm/{LL,LU,RL,RU}.hpp) against
+    oracle.symm; A's unread triangle is NaN."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        npdt = np.float64 if dtype == el.F64 else np.float32
+        for side in (el.LEFT, el.RIGHT):
+            for uplo in (el.LOWER, el.UPPER):
+                k = m if side == el.LEFT else n
+                Ag = oracle.hash_matrix(k, k, seed + 1, -0.1, 0.1, npdt)
+                i, j = np.indices((k, k))
+                Ag[(i < j) if uplo == el.LOWER else (i > j)] = np.nan
+                Bg = oracle.hash_matrix(m, n, seed + 2, -0.1, 0.1, npdt)
+                Cg = oracle.hash_matrix(m, n, seed + 3, -0.1, 0.1, npdt)
+                ref = oracle.symm("LR"[side], "LU"[uplo], 0.5, Ag, Bg, -0.5, Cg)
+                A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=k, width=k)
+                B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
+                C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
+                A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+                B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
+                C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                (el.Hemm if uplo else el.Symm)(side, uplo, 0.5, A, B, -0.5, C)
+                got = C.get_local().astype(np.float64)
+                want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank)
+                num = np.linalg.norm(got - want) if got.size else 0.0
+                Af = np.where(np.isnan(Ag), 0.0, Ag).astype(np.float64)
+                den = 2 * np.linalg.norm(Af) * np.linalg.norm(Bg.astype(np.float64)) * k * _tol(dtype)
+                assert np.isfinite(got).all() and num <= 10 * den, \
+                    f"Symm side {side} uplo {uplo} grid {r}x{c} rank {rank}: {num / den:.3g}"
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 def cannon_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, seed: int):
     """Cannon_NN (src/blas_like/level3/Gemm/NN.hpp:21-104) on a square grid with
     misaligned A, B and C (exercises the initial skew shifts), against the

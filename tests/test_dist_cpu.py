@@ -65,6 +65,12 @@ def test_trsm(world, height, outer, monkeypatch):
     _spawn(W.trsm_worker, world, height, el.CPU, el.F64, 19, 13, 4, 31)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1), (4, 2)])
+def test_symm_hemm(world, height):
+    """El::Symm / El::Hemm, LEFT/RIGHT x LOWER/UPPER; A's other triangle is NaN."""
+    _spawn(W.symm_worker, world, height, el.CPU, el.F64, 17, 11, 51)
+
+
 @pytest.mark.parametrize("world,height", [(1, 1), (4, 2), (2, 1)])
 def test_gemm_cannon(world, height):
     """Cannon_NN on 1x1 and 2x2 with random alignments; LogicError on a 2x1 grid,

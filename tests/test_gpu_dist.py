@@ -258,3 +258,9 @@ def test_gpu_trsm_large(dtype):
             ref = oracle.trsm("L", "LU"[uplo], "NT"[orient], "N", 1.0, Ag, Bg)
             err = np.linalg.norm(got - ref) / (np.linalg.norm(ref) * m * np.finfo(npdt).eps)
             assert err <= 10, (uplo, orient, err)
+
+
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1), (4, 2)])
+def test_gpu_symm_distributed(world, height):
+    """El::Symm / El::Hemm on the GPU (trapezoid copy + SUMMA), host-staged ranks."""
+    _spawn(W.symm_worker, world, height, el.GPU, el.F64, 45, 29, 61)
