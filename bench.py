@@ -14,6 +14,11 @@ Default workload (the driver's line):
   N = 1 : C2, El::Gemm NN fp64 m=n=k=32768 on a 1x1 grid (BASELINE.json configs[1]).
   N > 1 : C3, SUMMA El::Gemm NN fp64 m=n=k=65536 on Grid::DefaultHeight(N)
           (1x2, 2x2, 2x4): strong scaling of the same problem.
+  N = 1 also reports "c3_1gpu": C3's n = 65536 on the one GPU through the same
+          kc = 4096 panel path, the same-problem denominator for strong scaling.
+  N > 1 first checks the reference's associativity residual through the
+          distributed path (n = 4096) and reports xGMI GB/s from transfer-only
+          events plus the compute-stream gaps the panel pipeline left exposed.
 Extra lines (evidence, not the driver's default):
   --config c4 : TN fp32 m=n=8192, k=524288*N, inputs [VC,STAR] (LBANN's
                 weight-gradient shape, SUMMA_DOT); weak scaling, = C4 at N=8.
@@ -74,6 +79,110 @@ def measured_traffic(dtype: str, n: int, world: int):
     return ent["hbm_bytes_per_launch"] if ent else None
 
 
+def profile_summary(L, ctypes_mod):
+    """Event-timed stats of the profiled region: local MFMA launches, panel
+    transfers (whole redistribution incl. pack/unpack), RCCL transfers only,
+    and the compute-stream gaps between consecutive panel updates."""
+    c = ctypes_mod
+    gemm_ms, launches, flops = c.c_double(), c.c_int64(), c.c_double()
+    comm_ms, comm_bytes = c.c_double(), c.c_int64()
+    L.call("elx_profile_stats", c.byref(gemm_ms), c.byref(launches), c.byref(flops), c.byref(comm_ms),
+           c.byref(comm_bytes))
+    x_ms, x_bytes, x_n = c.c_double(), c.c_int64(), c.c_int64()
+    L.call("elx_profile_transfers", c.byref(x_ms), c.byref(x_bytes), c.byref(x_n))
+    gap_ms, gaps = c.c_double(), c.c_int64()
+    L.call("elx_profile_pipeline", c.byref(gap_ms), c.byref(gaps))
+    return {"gemm_ms": gemm_ms.value, "launches": launches.value, "flops": flops.value,
+            "redist_ms": comm_ms.value, "redist_bytes": comm_bytes.value,
+            "xfer_ms": x_ms.value, "xfer_bytes": x_bytes.value, "xfers": x_n.value,
+            "gap_ms": gap_ms.value, "gaps": gaps.value}
+
+
+def collectives_summary(prof: dict, steps: int) -> dict:
+    """Per-rank panel traffic: RCCL transfer-only GB/s (events around each grouped
+    send/recv; bytes = algorithmic bytes received), the whole redistribution time
+    (pack + transfer + unpack), and how much compute-stream time the pipeline
+    left exposed between panel updates."""
+    x = prof
+    return {
+        "bytes_per_rank_per_step": x["xfer_bytes"] // max(steps, 1),
+        "transfers_timed": x["xfers"],
+        "transfer_ms_per_rank": round(x["xfer_ms"], 3),
+        "GB_per_s": round(x["xfer_bytes"] / (x["xfer_ms"] * 1e-3) / 1e9, 2) if x["xfer_ms"] > 0 else None,
+        "redistribution_ms_per_rank": round(x["redist_ms"], 3),
+        "exposed_compute_gap_ms_per_step": round(x["gap_ms"] / max(steps, 1), 3),
+        "panel_gaps_timed": x["gaps"],
+    }
+
+
+def associativity_residual(el, grid, n: int = 4096, nrhs: int = 100) -> float:
+    """tests/blas_like/Gemm.cpp:15-49 on the distributed path itself (no oracle):
+    C_f = 0.5 A B - 0.5 C, then ||(0.5 A (B X) - 0.5 C X) - C_f X||_F / ||Y||_F
+    with every product an El::Gemm on this grid; norms on VC rank 0."""
+    import numpy as np
+    mk = lambda h, w, seed: el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=h, width=w).fill_hash(seed, 0.0, 0.1)
+    A, B, C, X = mk(n, n, 5), mk(n, n, 6), mk(n, n, 7), mk(n, nrhs, 8)
+    BX = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=nrhs)
+    Y = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=nrhs)
+    CX = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=nrhs)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, B, X, 0.0, BX)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, C, X, 0.0, CX)
+    el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, BX, 0.0, Y)
+    el.Axpy(-0.5, CX, Y)                                   # Y = 0.5 A B X - 0.5 C X
+    el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)     # C_f
+    E = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=nrhs)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, C, X, 0.0, E)
+    el.Axpy(-1.0, Y, E)                                    # E = C_f X - Y
+    out = []
+    for M in (E, Y):
+        R = el.DistMatrix(grid, el.F64, el.CIRC, el.CIRC, el.GPU)
+        R.assign(M)
+        out.append(R.get_local())
+    if grid.vc_rank != 0:
+        return float("nan")
+    return float(np.linalg.norm(out[0]) / np.linalg.norm(out[1]))
+
+
+def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n: int = 65536,
+               kc: int = 4096) -> dict:
+    """C3 (El::Gemm NN fp64 m=n=k=65536) on a 1x1 grid through the panel path:
+    k in kc-deep compute panels exactly as on the 1x2 / 2x2 / 2x4 grids (there the
+    panels are gathered; here they are views), so value_N / (N * value) is a
+    same-problem strong-scaling efficiency."""
+    el.SetComputePanel(kc)
+    try:
+        A = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(2, 0.0, 0.1)
+        C = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(3, 0.0, 0.1)
+        for _ in range(warmup):
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
+        barrier()
+        L.call("elx_set_profiling", 1)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        prof = profile_summary(L, ctypes)
+        L.call("elx_set_profiling", 0)
+    finally:
+        el.SetComputePanel(kc_restore)
+    value = 2.0 * n ** 3 * steps / elapsed / 1e12
+    avg_ms = prof["gemm_ms"] / max(prof["launches"], 1)
+    fpl = prof["flops"] / max(prof["launches"], 1)
+    ach = fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    return {"workload": f"C3 on 1 GPU: El::Gemm NN f64 m=n=k={n}, Grid 1x1, compute panel kc={kc} "
+                        f"({n // kc} MFMA launches per step)",
+            "value": round(value, 3), "unit": "TFLOP/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "pct_of_mfma_peak": round(100.0 * value / PEAK_TFLOPS["f64"], 2),
+            "roofline": {"bound": "mfma", "kernel": KERNEL["f64"], "achieved": round(ach, 3),
+                         "peak": PEAK_TFLOPS["f64"], "frac": round(ach / PEAK_TFLOPS["f64"], 4),
+                         "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)},
+            "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +194,10 @@ def main():
     ap.add_argument("--nb", type=int, default=128, help="El::Blocksize (communication panel)")
     ap.add_argument("--kc", type=int, default=0, help="compute panel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-residual", action="store_true", help="skip the N>1 associativity check")
+    ap.add_argument("--c3-steps", type=int, default=2, help="timed steps of the N=1 C3 point")
+    ap.add_argument("--no-c3-1gpu", action="store_true",
+                    help="N=1: skip the same-problem C3 point (n=65536 through the panel path)")
     args = ap.parse_args()
 
     import torch
@@ -144,6 +257,13 @@ def main():
     def step():
         return el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
 
+    residual = None
+    if world > 1 and not args.no_residual:
+        # correctness on this very grid before timing (no oracle): the reference's
+        # associativity check through the distributed path
+        residual = associativity_residual(el, grid)
+        barrier()
+
     for _ in range(args.warmup):
         step()
     barrier()
@@ -156,11 +276,7 @@ def main():
         alg = step()
     barrier()
     elapsed = time.perf_counter() - t0
-
-    gemm_ms, launches, flops = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-    comm_ms, comm_bytes = ctypes.c_double(), ctypes.c_int64()
-    L.call("elx_profile_stats", ctypes.byref(gemm_ms), ctypes.byref(launches), ctypes.byref(flops),
-           ctypes.byref(comm_ms), ctypes.byref(comm_bytes))
+    prof = profile_summary(L, ctypes)
     L.call("elx_set_profiling", 0)
 
     def max_over_ranks(x: float) -> float:
@@ -173,8 +289,8 @@ def main():
     elapsed = max_over_ranks(elapsed)
     total_flops = 2.0 * m * n * k * args.steps
     value = total_flops / elapsed / 1e12
-    avg_ms = gemm_ms.value / max(launches.value, 1)
-    flops_per_launch = flops.value / max(launches.value, 1)
+    avg_ms = prof["gemm_ms"] / max(prof["launches"], 1)
+    flops_per_launch = prof["flops"] / max(prof["launches"], 1)
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     peak = PEAK_TFLOPS[dtype]
     out = {
@@ -209,16 +325,15 @@ def main():
             "frac": round(achieved / peak, 4),
             "traffic": measured_traffic(dtype, m, world) if config in ("c2", "c3") else None,
             "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
-            "launches_timed": launches.value,
+            "launches_timed": prof["launches"],
             "avg_launch_ms": round(avg_ms, 3),
             "flops_per_launch": flops_per_launch,
         },
-        "collectives": {
-            "bytes_per_rank": comm_bytes.value,
-            "transfer_ms_per_rank": round(comm_ms.value, 3),
-            "GB_per_s": round(comm_bytes.value / (comm_ms.value * 1e-3) / 1e9, 2) if comm_ms.value > 0 else None,
-        },
+        "collectives": collectives_summary(prof, args.steps),
     }
+    if residual is not None:
+        out["residual"] = {"check": "associativity ||(aAB+bC)X - C_f X||_F/||Y||_F, n=4096, 100 rhs "
+                                    "(tests/blas_like/Gemm.cpp:15-49)", "value": residual, "ok": residual < 1e-13}
     if config == "c5":
         # DistMatrix Axpy / Hadamard on the [MC,MR] operands (no exchange: each
         # rank updates its local block); HBM bytes 3 x local elements x size
@@ -237,6 +352,11 @@ def main():
             ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
                         "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
         out["entrywise"] = ew
+    if world == 1 and config == "c2" and not args.n and not args.no_c3_1gpu:
+        # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 4096
+        # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
+        del A, B, C
+        out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libelemental_amd.so")
 
 # status codes / enums (mirrors include/elemental_amd.h)
-OK, ERR_LOGIC, ERR_HIP, ERR_COMM, ERR_RUNTIME, ERR_UNSUPPORTED, ERR_NO_DEVICE = range(7)
+OK, ERR_LOGIC, ERR_HIP, ERR_COMM, ERR_RUNTIME, ERR_UNSUPPORTED, ERR_NO_DEVICE, ERR_SINGULAR = range(8)
 NORMAL, TRANSPOSE, ADJOINT = 0, 1, 2
 MC, MD, MR, VC, VR, STAR, CIRC = range(7)
 (GEMM_DEFAULT, GEMM_SUMMA_A_MS, GEMM_SUMMA_A, GEMM_SUMMA_B_MS, GEMM_SUMMA_B, GEMM_SUMMA_C_MS,
@@ -59,6 +59,11 @@ _SIGS = {
     "elx_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, c_float, _vp, _i64, _vp, _i64, c_float, _vp, _i64, _vp]),
     "elx_gemm_f16": (_i, [_i, _i, _i64, _i64, _i64, c_float, _vp, _i64, _vp, _i64, c_float, _vp, _i64, _vp]),
     "elx_gemm_bf16": (_i, [_i, _i, _i64, _i64, _i64, c_float, _vp, _i64, _vp, _i64, c_float, _vp, _i64, _vp]),
+    "elx_matrix_gemm": (_i, [_i, _i, _i, _i, _i64, _i64, _i64, _d, _vp, _i64, _vp, _i64, _d, _vp, _i64, _vp]),
+    "elx_matrix_fill": (_i, [_i, _i, _i64, _i64, _d, _vp, _i64, _vp]),
+    "elx_matrix_scale": (_i, [_i, _i, _i64, _i64, _d, _vp, _i64, _vp]),
+    "elx_matrix_axpy": (_i, [_i, _i, _i64, _i64, _d, _vp, _i64, _vp, _i64, _vp]),
+    "elx_matrix_copy": (_i, [_i, _i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_axpy2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_copy2d": (_i, [_i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_copy2d_convert": (_i, [_i, _i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
@@ -72,6 +77,7 @@ _SIGS = {
     "elx_comm_unique_id": (_i, [POINTER(c_ubyte)]),
     "elx_comm_init_rccl": (_i, [POINTER(c_void_p), _i, _i, POINTER(c_ubyte)]),
     "elx_comm_init_host": (_i, [POINTER(c_void_p), _i, _i, HOST_COLL_FN, HOST_SPLIT_FN, _vp]),
+    "elx_comm_wrap_rccl": (_i, [POINTER(c_void_p), _vp]),
     "elx_comm_rank": (_i, [_vp, POINTER(c_int)]),
     "elx_comm_size": (_i, [_vp, POINTER(c_int)]),
     "elx_comm_destroy": (_i, [_vp]),
@@ -106,6 +112,10 @@ _SIGS = {
     "elx_dm_stream": (_i, [_vp, POINTER(c_void_p)]),
     "elx_dm_write": (_i, [_vp, c_char_p, _i, _i]),
     "elx_dm_read": (_i, [_vp, c_char_p, _i, _i]),
+    "elx_dm_get": (_i, [_vp, _i64, _i64, POINTER(c_double)]),
+    "elx_dm_set": (_i, [_vp, _i64, _i64, _d]),
+    "elx_dm_update": (_i, [_vp, _i64, _i64, _d]),
+    "elx_dm_fill": (_i, [_vp, _d]),
     "elx_dm_axpy": (_i, [_d, _vp, _vp]),
     "elx_dm_scale": (_i, [_d, _vp]),
     "elx_dm_zero": (_i, [_vp]),
@@ -118,7 +128,7 @@ _SIGS = {
     "elx_syrk": (_i, [_i, _i, _d, _vp, _d, _vp, _i]),
     "elx_trrk": (_i, [_i, _i, _i, _d, _vp, _vp, _d, _vp]),
     "elx_syr2k": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
-    "elx_trsm": (_i, [_i, _i, _i, _i, _d, _vp, _vp]),
+    "elx_trsm": (_i, [_i, _i, _i, _i, _d, _vp, _vp, _i]),
     "elx_symm": (_i, [_i, _i, _d, _vp, _vp, _d, _vp, _i]),
     "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
@@ -128,6 +138,8 @@ _SIGS = {
     "elx_set_profiling": (_i, [_i]),
     "elx_profile_stats": (_i, [POINTER(c_double), POINTER(c_int64), POINTER(c_double), POINTER(c_double),
                                POINTER(c_int64)]),
+    "elx_profile_transfers": (_i, [POINTER(c_double), POINTER(c_int64), POINTER(c_int64)]),
+    "elx_profile_pipeline": (_i, [POINTER(c_double), POINTER(c_int64)]),
 }
 
 
@@ -151,7 +163,12 @@ class NoDeviceError(ElxError):
     pass
 
 
-_EXC = {ERR_LOGIC: LogicError, ERR_UNSUPPORTED: UnsupportedError, ERR_NO_DEVICE: NoDeviceError}
+class SingularMatrixError(ElxError):
+    """El::SingularMatrixException (include/El/core/environment/decl.hpp:209-214)."""
+
+
+_EXC = {ERR_LOGIC: LogicError, ERR_UNSUPPORTED: UnsupportedError, ERR_NO_DEVICE: NoDeviceError,
+        ERR_SINGULAR: SingularMatrixError}
 
 _lib = None
 

@@ -118,6 +118,74 @@ ELX_GEMM_ENTRY(elx_gemm_f16, DType::F16, uint16_t, float)
 ELX_GEMM_ENTRY(elx_gemm_bf16, DType::BF16, uint16_t, float)
 #undef ELX_GEMM_ENTRY
 
+// ---- El::Matrix<T,D> (either device) ------------------------------------------
+namespace {
+hipStream_t DevStream(Device d, void* stream) { return d == Device::GPU ? S(stream) : nullptr; }
+void CheckLd(int64_t ld, int64_t rows, const char* what) {
+    ELX_REQUIRE(ld >= (rows > 1 ? rows : 1), what, " leading dimension ", ld, " < ", rows);
+}
+}  // namespace
+int elx_matrix_gemm(int dtype, int device, int opA, int opB, int64_t m, int64_t n, int64_t k, double alpha,
+                    const void* A, int64_t lda, const void* B, int64_t ldb, double beta, void* C, int64_t ldc,
+                    void* stream) {
+    return Guard([&] {
+        CheckOp(opA);
+        CheckOp(opB);
+        ELX_REQUIRE(m >= 0 && n >= 0 && k >= 0, "negative GEMM dimension");
+        const bool ta = opA != ELX_NORMAL, tb = opB != ELX_NORMAL;
+        CheckLd(ldc, m, "C");
+        CheckLd(lda, ta ? k : m, "A");
+        CheckLd(ldb, tb ? n : k, "B");
+        if (m == 0 || n == 0) return;
+        const Device d = ToDevice(device);
+        if (k == 0) {  // Gemm.cpp:240-248: C := beta C (beta == 0 clears NaNs)
+            if (beta == 0.0) exec::Fill(d, ToDType(dtype), m, n, 0.0, C, ldc, DevStream(d, stream));
+            else if (beta != 1.0) exec::Scale(d, ToDType(dtype), m, n, beta, C, ldc, DevStream(d, stream));
+            return;
+        }
+        exec::Gemm(d, ToDType(dtype), ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, DevStream(d, stream));
+    });
+}
+int elx_matrix_fill(int dtype, int device, int64_t m, int64_t n, double value, void* A, int64_t lda, void* stream) {
+    return Guard([&] {
+        CheckLd(lda, m, "A");
+        if (m == 0 || n == 0) return;
+        const Device d = ToDevice(device);
+        exec::Fill(d, ToDType(dtype), m, n, value, A, lda, DevStream(d, stream));
+    });
+}
+int elx_matrix_scale(int dtype, int device, int64_t m, int64_t n, double alpha, void* A, int64_t lda, void* stream) {
+    return Guard([&] {
+        CheckLd(lda, m, "A");
+        if (m == 0 || n == 0) return;
+        const Device d = ToDevice(device);
+        if (alpha == 0.0) exec::Fill(d, ToDType(dtype), m, n, 0.0, A, lda, DevStream(d, stream));
+        else if (alpha != 1.0) exec::Scale(d, ToDType(dtype), m, n, alpha, A, lda, DevStream(d, stream));
+    });
+}
+int elx_matrix_axpy(int dtype, int device, int64_t m, int64_t n, double alpha, const void* X, int64_t ldx, void* Y,
+                    int64_t ldy, void* stream) {
+    return Guard([&] {
+        CheckLd(ldx, m, "X");
+        CheckLd(ldy, m, "Y");
+        if (m == 0 || n == 0) return;
+        const Device d = ToDevice(device);
+        kern::Copy2D c{m, n, X, 1, ldx, Y, 1, ldy};
+        exec::Copy2DBatch(d, ToDType(dtype), &c, 1, true, alpha, DevStream(d, stream));
+    });
+}
+int elx_matrix_copy(int dtype, int device, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb,
+                    void* stream) {
+    return Guard([&] {
+        CheckLd(lda, m, "A");
+        CheckLd(ldb, m, "B");
+        if (m == 0 || n == 0) return;
+        const Device d = ToDevice(device);
+        kern::Copy2D c{m, n, A, 1, lda, B, 1, ldb};
+        exec::Copy2DBatch(d, ToDType(dtype), &c, 1, false, 0.0, DevStream(d, stream));
+    });
+}
+
 // ---- BLAS-1 --------------------------------------------------------------
 int elx_axpy2d(int dtype, int64_t m, int64_t n, double alpha, const void* X, int64_t xcs, int64_t xrs, void* Y,
                int64_t ycs, int64_t yrs, void* stream) {
@@ -189,6 +257,9 @@ int elx_comm_init_host(elx_comm_t* world, int rank, int size, elx_host_coll_fn c
     return Guard([&] {
         *world = new elx_comm_s{size == 1 && !coll ? Comm::Self() : Comm::InitHost(rank, size, coll, split, ctx)};
     });
+}
+int elx_comm_wrap_rccl(elx_comm_t* comm, void* nccl_comm) {
+    return Guard([&] { *comm = new elx_comm_s{Comm::WrapRCCL(static_cast<ncclComm_t>(nccl_comm))}; });
 }
 int elx_comm_rank(elx_comm_t c, int* rank) { return Guard([&] { *rank = c->c->Rank(); }); }
 int elx_comm_size(elx_comm_t c, int* size) { return Guard([&] { *size = c->c->Size(); }); }
@@ -298,6 +369,11 @@ int elx_dm_read(elx_dm_t A, const char* filename, int format, int int_bytes) {
     });
 }
 
+int elx_dm_get(elx_dm_t A, int64_t i, int64_t j, double* value) { return Guard([&] { *value = Get(M(A), i, j); }); }
+int elx_dm_set(elx_dm_t A, int64_t i, int64_t j, double value) { return Guard([&] { Set(M(A), i, j, value); }); }
+int elx_dm_update(elx_dm_t A, int64_t i, int64_t j, double value) { return Guard([&] { Update(M(A), i, j, value); }); }
+int elx_dm_fill(elx_dm_t A, double value) { return Guard([&] { Fill(M(A), value); }); }
+
 int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y) { return Guard([&] { Axpy(alpha, M(X), M(Y)); }); }
 int elx_dm_scale(double alpha, elx_dm_t A) { return Guard([&] { Scale(alpha, M(A)); }); }
 int elx_dm_zero(elx_dm_t A) { return Guard([&] { Zero(M(A)); }); }
@@ -343,10 +419,10 @@ int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double
         Syr2k(uplo, orient, alpha, M(A), M(B), beta, M(C));
     });
 }
-int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B) {
+int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B, int checkIfSingular) {
     return Guard([&] {
         CheckOp(orient);
-        Trsm(side, uplo, orient, diag, alpha, M(A), M(B));
+        Trsm(side, uplo, orient, diag, alpha, M(A), M(B), checkIfSingular != 0);
     });
 }
 int elx_symm(int side, int uplo, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C, int conjugate) {
@@ -364,5 +440,9 @@ int elx_set_profiling(int on) { return Guard([&] { SetProfiling(on != 0); }); }
 int elx_profile_stats(double* gemm_ms, int64_t* launches, double* flops, double* comm_ms, int64_t* bytes) {
     return Guard([&] { ProfileStats(*gemm_ms, *launches, *flops, *comm_ms, *bytes); });
 }
+int elx_profile_transfers(double* transfer_ms, int64_t* bytes, int64_t* transfers) {
+    return Guard([&] { CommProfileStats(*transfer_ms, *bytes, *transfers); });
+}
+int elx_profile_pipeline(double* gap_ms, int64_t* gaps) { return Guard([&] { PipelineStats(*gap_ms, *gaps); }); }
 
 }  // extern "C"

@@ -10,6 +10,48 @@ CommStats& GlobalCommStats() {
     return s;
 }
 
+CommProfiler& CommProf() {
+    static CommProfiler p;
+    return p;
+}
+
+void CommProfiler::Clear() {
+    for (auto& r : recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    recs.clear();
+}
+
+CommProfiler::Rec CommProfiler::Begin(hipStream_t s) {
+    Rec r;
+    if (!on || !s) return r;
+    ELX_CHECK_HIP(hipEventCreate(&r.a));
+    ELX_CHECK_HIP(hipEventCreate(&r.b));
+    ELX_CHECK_HIP(hipEventRecord(r.a, s));
+    return r;
+}
+
+void CommProfiler::End(Rec r, hipStream_t s, int64_t bytes) {
+    if (!r.a) return;
+    ELX_CHECK_HIP(hipEventRecord(r.b, s));
+    r.bytes = bytes;
+    recs.push_back(r);
+}
+
+void CommProfiler::Stats(double& ms, int64_t& bytes, int64_t& calls) {
+    ms = 0;
+    bytes = calls = 0;
+    for (auto& r : recs) {
+        ELX_CHECK_HIP(hipEventSynchronize(r.b));
+        float t = 0;
+        ELX_CHECK_HIP(hipEventElapsedTime(&t, r.a, r.b));
+        ms += t;
+        bytes += r.bytes;
+        ++calls;
+    }
+}
+
 namespace {
 
 ncclDataType_t NcclType(DType t) {
@@ -67,6 +109,18 @@ std::shared_ptr<Comm> Comm::InitRCCL(int rank, int size, const unsigned char id[
     return c;
 }
 
+std::shared_ptr<Comm> Comm::WrapRCCL(ncclComm_t nc) {
+    ELX_REQUIRE(nc != nullptr, "null RCCL communicator");
+    Runtime::Get().EnsureGPU();
+    auto c = std::shared_ptr<Comm>(new Comm());
+    c->kind_ = Kind::RCCL;
+    c->nccl_ = nc;
+    c->owned_ = false;
+    CheckNccl(ncclCommUserRank(nc, &c->rank_), "ncclCommUserRank");
+    CheckNccl(ncclCommCount(nc, &c->size_), "ncclCommCount");
+    return c;
+}
+
 std::shared_ptr<Comm> Comm::InitHost(int rank, int size, elx_host_coll_fn coll, elx_host_split_fn split, void* ctx) {
     ELX_REQUIRE(coll != nullptr, "host comm needs a collective callback");
     ELX_REQUIRE(rank >= 0 && rank < size, "bad rank ", rank, " of ", size);
@@ -82,7 +136,7 @@ std::shared_ptr<Comm> Comm::InitHost(int rank, int size, elx_host_coll_fn coll, 
 }
 
 Comm::~Comm() {
-    if (nccl_) (void)ncclCommDestroy(nccl_);
+    if (nccl_ && owned_) (void)ncclCommDestroy(nccl_);
 }
 
 std::shared_ptr<Comm> Comm::Split(int color, int key) {
@@ -149,6 +203,7 @@ void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Devic
         CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclReduceScatter");
         return;
     }
+    if (t == DType::F16 || t == DType::BF16) { HostSum16(true, t, send, recv, count, dev, s); return; }
     if (dev == Device::CPU) { HostCall(ELX_COLL_REDUCE_SCATTER, t, send, recv, count, 0, 0); return; }
     static Staging stg;
     char* h = static_cast<char*>(stg.Get(bytes * (size_ + 1)));
@@ -168,6 +223,7 @@ void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device de
         CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclAllReduce");
         return;
     }
+    if (t == DType::F16 || t == DType::BF16) { HostSum16(false, t, send, recv, count, dev, s); return; }
     if (dev == Device::CPU) { HostCall(ELX_COLL_ALLREDUCE, t, send, recv, count, 0, 0); return; }
     static Staging stg;
     char* h = static_cast<char*>(stg.Get(bytes * 2));
@@ -176,6 +232,35 @@ void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device de
     HostCall(ELX_COLL_ALLREDUCE, t, h, h + bytes, count, 0, 0);
     ELX_CHECK_HIP(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, s));
     ELX_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+// Every rank gathers the contributions it reduces (ALLTOALL of its slice for
+// a reduce-scatter, ALLGATHER for an all-reduce) and folds them in rank order,
+// each addition done in float and rounded back to 16 bits, as
+// GPUHalfSumFunc's out[i] = float(in[i]) + float(out[i]) (environment.cpp:135-142).
+void Comm::HostSum16(bool scatter, DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+    const size_t es = DTypeSize(t);
+    const Int sendCount = scatter ? count * size_ : count;
+    std::vector<uint16_t> hs(static_cast<size_t>(sendCount)), hr(static_cast<size_t>(count) * size_);
+    if (dev == Device::GPU) {
+        ELX_CHECK_HIP(hipMemcpyAsync(hs.data(), send, sendCount * es, hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(hs.data(), send, sendCount * es);
+    }
+    HostCall(scatter ? ELX_COLL_ALLTOALL : ELX_COLL_ALLGATHER, t, hs.data(), hr.data(), count, 0, 0);
+    const bool bf = t == DType::BF16;
+    auto ld = [&](uint16_t v) { return bf ? BF16ToFloat(v) : HalfToFloat(v); };
+    auto st = [&](float v) { return bf ? FloatToBF16(v) : FloatToHalf(v); };
+    std::vector<uint16_t> out(hr.begin(), hr.begin() + count);
+    for (int r = 1; r < size_; ++r)
+        for (Int i = 0; i < count; ++i) out[i] = st(ld(hr[r * count + i]) + ld(out[i]));
+    if (dev == Device::GPU) {
+        ELX_CHECK_HIP(hipMemcpyAsync(recv, out.data(), count * es, hipMemcpyHostToDevice, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(recv, out.data(), count * es);
+    }
 }
 
 void Comm::Bcast(DType t, void* buf, Int count, int root, Device dev, hipStream_t s) {
@@ -213,6 +298,10 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
         const ncclDataType_t nt = NcclType(t);
+        int64_t in_bytes = 0;
+        for (int q = 0; q < size_; ++q)
+            if (q != rank_) in_bytes += static_cast<int64_t>(rc[q] * es);
+        auto rec = CommProf().Begin(s);
         CheckNccl(ncclGroupStart(), "ncclGroupStart");
         for (int q = 0; q < size_; ++q) {
             if (q == rank_) continue;
@@ -220,6 +309,7 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
             if (rc[q] > 0) CheckNccl(ncclRecv(rb + rd[q] * es, rc[q], nt, q, nccl_, s), "ncclRecv");
         }
         CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+        CommProf().End(rec, s, in_bytes);
         return;
     }
     // host backend: uniform-count all-to-all padded to the largest pair

@@ -29,12 +29,28 @@ struct CommStats {
 };
 CommStats& GlobalCommStats();
 
+// Transfer-only timing of device collectives (HIP events on the stream the
+// RCCL group runs on; pack/unpack launches excluded): the xGMI GB/s figure.
+struct CommProfiler {
+    struct Rec { hipEvent_t a = nullptr, b = nullptr; int64_t bytes = 0; };
+    bool on = false;
+    std::vector<Rec> recs;
+    void Clear();
+    Rec Begin(hipStream_t s);
+    void End(Rec r, hipStream_t s, int64_t bytes);
+    // summed transfer ms, bytes received, number of timed transfers
+    void Stats(double& ms, int64_t& bytes, int64_t& calls);
+};
+CommProfiler& CommProf();
+
 class Comm {
 public:
     enum class Kind { SELF, RCCL, HOST };
 
     static std::shared_ptr<Comm> Self();
     static std::shared_ptr<Comm> InitRCCL(int rank, int size, const unsigned char id[128]);
+    // borrow a caller's RCCL communicator (never destroyed here); splits of it are owned
+    static std::shared_ptr<Comm> WrapRCCL(ncclComm_t c);
     static std::shared_ptr<Comm> InitHost(int rank, int size, elx_host_coll_fn coll, elx_host_split_fn split,
                                           void* ctx);
     ~Comm();
@@ -63,9 +79,13 @@ public:
 private:
     Comm() = default;
     void HostCall(int op, DType t, const void* send, void* recv, Int count, int peer, int peer2);
+    // 16-bit sums on the host backend, independent of what the callback supports
+    // (the reference registers its own MPI_Op, src/core/environment.cpp:135-142,259-298)
+    void HostSum16(bool scatter, DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
     Kind kind_ = Kind::SELF;
     int rank_ = 0, size_ = 1;
     ncclComm_t nccl_ = nullptr;
+    bool owned_ = true;
     elx_host_coll_fn coll_ = nullptr;
     elx_host_split_fn split_ = nullptr;
     void* ctx_ = nullptr;

@@ -22,6 +22,10 @@ struct HIPError : std::runtime_error { using std::runtime_error::runtime_error; 
 struct CommError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct UnsupportedError : std::logic_error { using std::logic_error::logic_error; };
 struct NoDeviceError : std::runtime_error { using std::runtime_error::runtime_error; };
+// El::SingularMatrixException (include/El/core/environment/decl.hpp:209-214)
+struct SingularMatrixError : std::runtime_error {
+    SingularMatrixError() : std::runtime_error("Matrix was singular") {}
+};
 
 template <typename... Args>
 std::string Cat(Args&&... args) {
@@ -56,6 +60,7 @@ int Guard(F&& f) {
     catch (const HIPError& e)           { SetLastError(e.what()); return ELX_ERR_HIP; }
     catch (const CommError& e)          { SetLastError(e.what()); return ELX_ERR_COMM; }
     catch (const NoDeviceError& e)      { SetLastError(e.what()); return ELX_ERR_NO_DEVICE; }
+    catch (const SingularMatrixError& e) { SetLastError(e.what()); return ELX_ERR_SINGULAR; }
     catch (const std::logic_error& e)   { SetLastError(e.what()); return ELX_ERR_LOGIC; }
     catch (const std::exception& e)     { SetLastError(e.what()); return ELX_ERR_RUNTIME; }
     catch (...)                         { SetLastError("unknown exception"); return ELX_ERR_RUNTIME; }

@@ -319,6 +319,11 @@ std::shared_ptr<DistMatrix> DistMatrix::Like(Dist cd, Dist rd) const {
     return B;
 }
 
+std::shared_ptr<DistMatrix> DistMatrix::LikeOn(Dist cd, Dist rd, Device dev) const {
+    if (dev == dev_) return Like(cd, rd);
+    return std::make_shared<DistMatrix>(grid_, dtype_, cd, rd, dev, cd == cdist_ && rd == rdist_ ? root_ : 0);
+}
+
 void DistMatrix::SetLocal(const void* host, Int ld) {
     if (lh_ == 0 || lw_ == 0) return;
     ELX_REQUIRE(ld >= lh_, "leading dimension ", ld, " < local height ", lh_);

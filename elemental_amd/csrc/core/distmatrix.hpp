@@ -137,6 +137,8 @@ public:
     static std::shared_ptr<DistMatrix> View(const DistMatrix& A, Int i0, Int i1, Int j0, Int j1);
     // fresh matrix with the same grid/type/device
     std::shared_ptr<DistMatrix> Like(Dist cd, Dist rd) const;
+    // same grid/type on device `dev` (this matrix's stream when the device matches)
+    std::shared_ptr<DistMatrix> LikeOn(Dist cd, Dist rd, Device dev) const;
 
     // host <-> local block
     void SetLocal(const void* host, Int ld);

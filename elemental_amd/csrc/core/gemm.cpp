@@ -27,6 +27,7 @@
 #include "exec.hpp"
 #include <algorithm>
 #include <functional>
+#include <initializer_list>
 #include <vector>
 
 namespace elx {
@@ -52,8 +53,9 @@ bool IsN(int o) { return o == ELX_NORMAL; }
 
 // Event-bracketed profiling of the local updates and panel transfers.
 struct Profiler {
-    struct Rec { hipEvent_t a, b; double work; };
+    struct Rec { hipEvent_t a, b; double work; int call = -1; };
     bool on = false;
+    int calls = 0;  // SummaC invocations (groups consecutive panel updates)
     std::vector<Rec> gemm, comm;
     void Clear() {
         for (auto* v : {&gemm, &comm})
@@ -68,9 +70,10 @@ struct Profiler {
         ELX_CHECK_HIP(hipEventRecord(r.a, s));
         return r;
     }
-    void End(Rec r, hipStream_t s, double work, std::vector<Rec>& into) {
+    void End(Rec r, hipStream_t s, double work, std::vector<Rec>& into, int call = -1) {
         ELX_CHECK_HIP(hipEventRecord(r.b, s));
         r.work = work;
+        r.call = call;
         into.push_back(r);
     }
 };
@@ -88,14 +91,47 @@ void FenceStreams(hipStream_t from, hipStream_t to) {
     ELX_CHECK_HIP(hipEventDestroy(ev));
 }
 
-// DistMatrixReadProxy: A itself when it already has dist (cd,rd) [and the
-// requested alignment], else a redistributed copy.
-std::shared_ptr<const DistMatrix> ReadProxy(const DistMatrix& A, Dist cd, Dist rd, int calign = -1,
-                                            int ralign = -1) {
-    const bool ok = A.ColDist() == cd && A.RowDist() == rd && (calign < 0 || A.ColAlign() == calign) &&
-                    (ralign < 0 || A.RowAlign() == ralign);
-    if (ok) return std::shared_ptr<const DistMatrix>(&A, [](const DistMatrix*) {});
-    auto T = A.Like(cd, rd);
+// MultiSync (include/hydrogen/MultiSync.hpp:33-78): on entry the master stream
+// waits for the others' queued work; on exit the others wait for the master, so
+// a caller that reuses A or B on its own stream, and every temporary released
+// on those streams, is ordered after the reads issued here.
+class MultiSync {
+public:
+    MultiSync(hipStream_t master, std::initializer_list<hipStream_t> others) : master_(master), others_(others) {
+        for (hipStream_t o : others_) FenceStreams(o, master_);
+    }
+    ~MultiSync() {
+        for (hipStream_t o : others_) {
+            try { FenceStreams(master_, o); } catch (...) {}
+        }
+    }
+    MultiSync(const MultiSync&) = delete;
+    MultiSync& operator=(const MultiSync&) = delete;
+
+private:
+    hipStream_t master_;
+    std::vector<hipStream_t> others_;
+};
+
+// DistMatrixReadProxy<T,T,cd,rd,ELEMENT,D> (include/El/core/Proxy.hpp:174-300):
+// the operands are brought to the device of `tgt` (the matrix being written,
+// as Gemm/NN.hpp:357-359 proxies A and B onto C's device) and every read is
+// queued on tgt's stream.  A itself (as a view on that stream) when it already
+// has dist (cd,rd), that device [and the requested alignment]; else a
+// redistributed copy, moved across devices when needed.
+std::shared_ptr<const DistMatrix> ReadProxy(const DistMatrix& A, const DistMatrix& tgt, Dist cd, Dist rd,
+                                            int calign = -1, int ralign = -1) {
+    const bool ok = A.Dev() == tgt.Dev() && A.ColDist() == cd && A.RowDist() == rd &&
+                    (calign < 0 || A.ColAlign() == calign) && (ralign < 0 || A.RowAlign() == ralign);
+    if (ok) {
+        if (A.Dev() != Device::GPU || A.Stream() == tgt.Stream())
+            return std::shared_ptr<const DistMatrix>(&A, [](const DistMatrix*) {});
+        auto V = DistMatrix::View(A, 0, A.Height(), 0, A.Width());
+        V->SetStream(tgt.Stream());
+        return V;
+    }
+    auto T = A.LikeOn(cd, rd, tgt.Dev());
+    T->SetStream(tgt.Stream());
     if (calign >= 0) T->AlignCols(calign, true);
     if (ralign >= 0) T->AlignRows(ralign, true);
     Copy(A, *T);
@@ -245,8 +281,9 @@ void TrrkLocal(bool lower, bool ta, bool tb, Int k, double alpha, const void* a,
 // upper (ELX_UPPER) triangle is updated, through TrrkLocal.
 void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
             DistMatrix& CPre, int uplo = -1) {
-    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
-    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
+    auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
     const DistMatrix& A = *Ap;
     const DistMatrix& B = *Bp;
@@ -288,6 +325,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         }
     }
     const int np = static_cast<int>((K + kc - 1) / kc);
+    const int call_id = Prof().calls++;
     Buffer trrk_tmp;
 
     auto issue = [&](int p) {
@@ -329,7 +367,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             else
                 exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, a.Buffer(), a.LDim(), b.Buffer(),
                            b.LDim(), b_p, C.Buffer(), C.LDim(), cs);
-            if (prof) Prof().End(rec, cs, 2.0 * m * n * k, Prof().gemm);
+            if (prof) Prof().End(rec, cs, 2.0 * m * n * k, Prof().gemm, call_id);
         } else if (p == 0) {
             Scale(beta, C);
         }
@@ -364,8 +402,9 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // TN.hpp:19-61, TT.hpp:17-61.  Loop over column panels of C.
 // ---------------------------------------------------------------------------
 void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
-    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
-    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
+    auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
     const DistMatrix& A = *Ap;
     const DistMatrix& B = *Bp;
@@ -404,8 +443,9 @@ void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // NT.hpp:134-176, TN.hpp:137-176, TT.hpp:105-152.  Loop over row panels of C.
 // ---------------------------------------------------------------------------
 void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
-    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
-    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR);
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
+    auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
     const DistMatrix& A = *Ap;
     const DistMatrix& B = *Bp;
@@ -447,10 +487,12 @@ void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
               Int bs) {
     const Int m = CPre.Height(), n = CPre.Width();
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     // k must be distributed VC on both: op(A) = A ([*,VC]) or A^T ([VC,*])
-    auto Ap = IsN(oA) ? ReadProxy(APre, Dist::STAR, Dist::VC) : ReadProxy(APre, Dist::VC, Dist::STAR);
+    auto Ap = IsN(oA) ? ReadProxy(APre, CPre, Dist::STAR, Dist::VC) : ReadProxy(APre, CPre, Dist::VC, Dist::STAR);
     const int kAlign = IsN(oA) ? Ap->RowAlign() : Ap->ColAlign();
-    auto Bp = IsN(oB) ? ReadProxy(BPre, Dist::VC, Dist::STAR, kAlign, -1) : ReadProxy(BPre, Dist::STAR, Dist::VC, -1, kAlign);
+    auto Bp = IsN(oB) ? ReadProxy(BPre, CPre, Dist::VC, Dist::STAR, kAlign, -1)
+                      : ReadProxy(BPre, CPre, Dist::STAR, Dist::VC, -1, kAlign);
     RWProxy Cp(CPre);
     const DistMatrix& A = *Ap;
     const DistMatrix& B = *Bp;
@@ -481,11 +523,12 @@ void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMa
 void Cannon(double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
     const Grid& g = CPre.G();
     if (g.Height() != g.Width()) throw LogicError("Process grid must be square for Cannon's");
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     RWProxy Cp(CPre);
     DistMatrix& C = Cp.Get();
     // A aligned with C's rows, B with C's columns (NN.hpp:43-48)
-    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR, C.ColAlign(), -1);
-    auto Bp = ReadProxy(BPre, Dist::MC, Dist::MR, -1, C.RowAlign());
+    auto Ap = ReadProxy(APre, C, Dist::MC, Dist::MR, C.ColAlign(), -1);
+    auto Bp = ReadProxy(BPre, C, Dist::MC, Dist::MR, -1, C.RowAlign());
     const DistMatrix& A = *Ap;
     const DistMatrix& B = *Bp;
     const int q = g.Height();
@@ -493,10 +536,6 @@ void Cannon(double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMa
     const Device dev = C.Dev();
     const DType t = C.Type();
     hipStream_t s = C.Stream();
-    if (dev == Device::GPU) {
-        FenceStreams(A.Stream(), s);
-        FenceStreams(B.Stream(), s);
-    }
     const Int lhA = A.LocalHeight(), lwA = A.LocalWidth(), lhB = B.LocalHeight(), lwB = B.LocalWidth();
     const Int sizeA = lhA * lwA, sizeB = lhB * lwB;
     const size_t es = DTypeSize(t);
@@ -531,10 +570,6 @@ void Cannon(double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMa
                        std::max<Int>(lhB, 1), 1.0, C.Buffer(), C.LDim(), s);
         if (step != q - 1) shift(leftCol, rightCol, aboveRow, belowRow);
     }
-    if (dev == Device::GPU) {
-        FenceStreams(s, A.Stream());  // the packages are freed on s; the proxies' owners may reuse A/B
-        FenceStreams(s, B.Stream());
-    }
     Cp.Finish();
 }
 
@@ -558,6 +593,33 @@ void SetProfiling(bool on) {
     if (Runtime::Get().GPUInitialized()) ELX_CHECK_HIP(hipDeviceSynchronize());
     Prof().Clear();
     Prof().on = on;
+    CommProf().Clear();
+    CommProf().on = on;
+}
+
+void CommProfileStats(double& transfer_ms, int64_t& bytes, int64_t& transfers) {
+    transfer_ms = 0;
+    bytes = transfers = 0;
+    if (!Runtime::Get().GPUInitialized()) return;
+    CommProf().Stats(transfer_ms, bytes, transfers);
+}
+
+// Compute-stream idle time between consecutive panel updates of one SummaC
+// call: the time the MFMA stream waited for a panel gather the pipeline did not
+// hide (0 when every transfer overlapped the previous update).
+void PipelineStats(double& gap_ms, int64_t& gaps) {
+    gap_ms = 0;
+    gaps = 0;
+    if (!Runtime::Get().GPUInitialized()) return;
+    ELX_CHECK_HIP(hipDeviceSynchronize());
+    const auto& g = Prof().gemm;
+    for (size_t i = 1; i < g.size(); ++i) {
+        if (g[i].call < 0 || g[i].call != g[i - 1].call) continue;
+        float ms = 0;
+        ELX_CHECK_HIP(hipEventElapsedTime(&ms, g[i - 1].b, g[i].a));
+        gap_ms += ms > 0 ? ms : 0;
+        ++gaps;
+    }
 }
 
 void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& comm_ms, int64_t& bytes) {
@@ -602,11 +664,8 @@ void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatr
     }
     const bool prof = C.Dev() == Device::GPU && Prof().on;
     Profiler::Rec rec{};
-    if (C.Dev() == Device::GPU) {
-        FenceStreams(A.Stream(), C.Stream());
-        FenceStreams(B.Stream(), C.Stream());
-        if (prof) rec = Prof().Begin(C.Stream());
-    }
+    MultiSync sync(C.Stream(), {A.Stream(), B.Stream()});
+    if (prof) rec = Prof().Begin(C.Stream());
     exec::Gemm(C.Dev(), C.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
                beta, C.Buffer(), C.LDim(), C.Stream());
     if (prof) Prof().End(rec, C.Stream(), 2.0 * m * n * k, Prof().gemm);
@@ -707,7 +766,8 @@ Int TrsmOuter() {  // ELX_TRSM_OUTER overrides (tests: several outer blocks at s
 }
 
 void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatrix& XPre) {
-    auto Ap = ReadProxy(APre, Dist::MC, Dist::MR);
+    MultiSync sync(XPre.Stream(), {APre.Stream()});
+    auto Ap = ReadProxy(APre, XPre, Dist::MC, Dist::MR);
     const DistMatrix& A = *Ap;
     RWProxy Xp(XPre);
     DistMatrix& X = Xp.Get();
@@ -789,7 +849,8 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     Xp.Finish();
 }
 
-void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B) {
+void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B,
+          bool checkIfSingular) {
     ELX_REQUIRE(side == ELX_LEFT || side == ELX_RIGHT, "Trsm: bad LeftOrRight ", side);
     ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Trsm: bad UpperOrLower ", uplo);
     ELX_REQUIRE(orient >= ELX_NORMAL && orient <= ELX_ADJOINT, "Trsm: bad orientation");
@@ -799,6 +860,7 @@ void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatr
     if (A.Type() != DType::F64 && A.Type() != DType::F32) throw LogicError("Trsm: only float and double are supported");
     if (A.Height() != A.Width()) throw LogicError("A must be square");  // Trsm.cpp:142-143
     if ((side == ELX_LEFT ? B.Height() : B.Width()) != A.Height()) throw LogicError("Nonconformal Trsm");
+    if (checkIfSingular && diag != ELX_UNIT && DiagonalHasZero(A)) throw SingularMatrixError();
     Scale(alpha, B);  // Trsm.cpp:155 (B *= alpha)
     if (side == ELX_LEFT) return TrsmLeft(uplo, orient, diag == ELX_UNIT, A, B);
     auto Bt = B.Like(Dist::MC, Dist::MR);

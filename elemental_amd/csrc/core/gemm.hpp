@@ -25,7 +25,9 @@ void Trrk(int uplo, int oA, int oB, double alpha, const DistMatrix& A, const Dis
 void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMatrix& B, double beta,
            DistMatrix& C);
 // B := alpha op(A)^-1 B (LEFT) / alpha B op(A)^-1 (RIGHT)  (Trsm.cpp:129-420)
-void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B);
+// checkIfSingular: SingularMatrixError when a NON_UNIT diagonal holds an exact zero (Trsm.cpp:60-68)
+void Trsm(int side, int uplo, int orient, int diag, double alpha, const DistMatrix& A, DistMatrix& B,
+          bool checkIfSingular = false);
 // C := alpha A B + beta C (LEFT) / alpha B A + beta C (RIGHT), A symmetric (uplo stored)  (Symm.cpp:55-80)
 void Symm(int side, int uplo, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C);
 
@@ -36,5 +38,7 @@ Int ComputePanel();
 int LastGemmAlgorithm();
 void SetProfiling(bool on);
 void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& comm_ms, int64_t& bytes);
+void CommProfileStats(double& transfer_ms, int64_t& bytes, int64_t& transfers);
+void PipelineStats(double& gap_ms, int64_t& gaps);
 
 }  // namespace elx

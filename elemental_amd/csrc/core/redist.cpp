@@ -20,6 +20,7 @@
 // result is bit-exact by construction (pure data movement).
 #include "redist.hpp"
 #include "exec.hpp"
+#include <cstring>
 #include <numeric>
 #include <vector>
 
@@ -441,6 +442,147 @@ void Combine(int fn, const DistMatrix& A, DistMatrix& B) {
     Fence(A, B);
     exec::Combine(B.Dev(), B.Type(), fn, B.LocalHeight(), B.LocalWidth(), A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
                   B.Stream());
+}
+
+// ---------------------------------------------------------------------------
+// Entry access (ElementMatrix/setup.hpp:463-610) and grid-wide scalars.
+// ---------------------------------------------------------------------------
+namespace {
+
+// one double through a grid communicator: device buffers when the comm is RCCL
+template <typename F>
+double ScalarColl(const Grid& g, double v, F&& coll) {
+    if (g.Size() == 1) return v;
+    if (g.CommDevice() == Device::GPU) {
+        hipStream_t s = Runtime::Get().CommStream();
+        elx::Buffer b(Device::GPU, sizeof(double), s);
+        ELX_CHECK_HIP(hipMemcpyAsync(b.data(), &v, sizeof(double), hipMemcpyHostToDevice, s));
+        coll(b.data(), Device::GPU, s);
+        ELX_CHECK_HIP(hipMemcpyAsync(&v, b.data(), sizeof(double), hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+        return v;
+    }
+    coll(&v, Device::CPU, nullptr);
+    return v;
+}
+
+// does rank vc hold global entry (i, j) of A?
+bool HoldsOf(const DistMatrix& A, int vc, Int i, Int j) {
+    if (!A.ParticipatingOf(vc)) return false;
+    const Int cs = Shift(A.ColRankOf(vc), A.ColAlign(), A.ColStride());
+    const Int rs = Shift(A.RowRankOf(vc), A.RowAlign(), A.RowStride());
+    return Mod(i - cs, A.ColStride()) == 0 && Mod(j - rs, A.RowStride()) == 0;
+}
+
+char* LocalEntry(const DistMatrix& A, Int i, Int j) {
+    const Int iLoc = (i - A.ColShift()) / A.ColStride(), jLoc = (j - A.RowShift()) / A.RowStride();
+    return At(A, iLoc, jLoc);
+}
+
+double ReadEntry(const DistMatrix& A, const char* p) {
+    alignas(8) unsigned char tmp[8];
+    const size_t es = A.ElemSize();
+    if (A.Dev() == Device::GPU) {
+        ELX_CHECK_HIP(hipMemcpyAsync(tmp, p, es, hipMemcpyDeviceToHost, A.Stream()));
+        ELX_CHECK_HIP(hipStreamSynchronize(A.Stream()));
+    } else {
+        std::memcpy(tmp, p, es);
+    }
+    return exec::LoadScalar(A.Type(), tmp);
+}
+
+void WriteEntry(DistMatrix& A, char* p, double v) {
+    alignas(8) unsigned char tmp[8];
+    exec::StoreScalar(A.Type(), tmp, v);
+    const size_t es = A.ElemSize();
+    if (A.Dev() == Device::GPU) {
+        ELX_CHECK_HIP(hipMemcpyAsync(p, tmp, es, hipMemcpyHostToDevice, A.Stream()));
+        ELX_CHECK_HIP(hipStreamSynchronize(A.Stream()));
+    } else {
+        std::memcpy(p, tmp, es);
+    }
+}
+
+void CheckIndex(const DistMatrix& A, Int i, Int j) {
+    ELX_REQUIRE(i >= 0 && i < A.Height() && j >= 0 && j < A.Width(), "entry (", i, ",", j,
+                ") out of bounds of ", A.Height(), " x ", A.Width());
+}
+
+}  // namespace
+
+double GridAllReduceSum(const Grid& g, double v) {
+    return ScalarColl(g, v, [&](void* p, Device d, hipStream_t s) { g.VC().AllReduce(DType::F64, p, p, 1, d, s); });
+}
+
+double GridBcast(const Grid& g, double v, int rootVC) {
+    return ScalarColl(g, v, [&](void* p, Device d, hipStream_t s) { g.VC().Bcast(DType::F64, p, 1, rootVC, d, s); });
+}
+
+// El::DistMatrix::Get (ElementMatrix/setup.hpp:463-490): collective over the
+// grid; the lowest VC rank holding (i, j) reads it and broadcasts it.
+double Get(const DistMatrix& A, Int i, Int j) {
+    CheckIndex(A, i, j);
+    const Grid& g = A.G();
+    int owner = -1;
+    for (int q = 0; q < g.Size() && owner < 0; ++q)
+        if (HoldsOf(A, q, i, j)) owner = q;
+    double v = 0.0;
+    if (owner == g.VCRank()) v = ReadEntry(A, LocalEntry(A, i, j));
+    return GridBcast(g, v, owner);
+}
+
+// El::DistMatrix::Set / Update (setup.hpp:552-604): every rank holding (i, j)
+// writes its copy; no communication.
+void Set(DistMatrix& A, Int i, Int j, double v) {
+    CheckIndex(A, i, j);
+    if (HoldsOf(A, A.G().VCRank(), i, j)) WriteEntry(A, LocalEntry(A, i, j), v);
+}
+
+void Update(DistMatrix& A, Int i, Int j, double v) {
+    CheckIndex(A, i, j);
+    if (!HoldsOf(A, A.G().VCRank(), i, j)) return;
+    char* p = LocalEntry(A, i, j);
+    WriteEntry(A, p, ReadEntry(A, p) + v);
+}
+
+// El::Fill (include/El/blas_like/level1/Fill.hpp:20-70): every local entry := v
+void Fill(DistMatrix& A, double v) {
+    if (A.LocalHeight() == 0 || A.LocalWidth() == 0) return;
+    exec::Fill(A.Dev(), A.Type(), A.LocalHeight(), A.LocalWidth(), v, A.Buffer(), A.LDim(), A.Stream());
+}
+
+// Trsm's checkIfSingular (src/blas_like/level3/Trsm.cpp:60-68): is any diagonal
+// entry of A exactly zero?  The local diagonal entries form one arithmetic
+// progression (global index step lcm(colStride, rowStride)), gathered by one
+// strided copy; the per-rank answers are summed over the grid.
+bool DiagonalHasZero(const DistMatrix& A) {
+    const Int n = std::min(A.Height(), A.Width());
+    double zeros = 0;
+    if (A.Participating() && n > 0) {
+        const Int cs = A.ColShift(), rs = A.RowShift(), cstr = A.ColStride(), rstr = A.RowStride();
+        const Int L = cstr / Gcd(cstr, rstr) * rstr;
+        Int z = -1;
+        for (Int t = cs; t < cs + L; t += cstr)
+            if (Mod(t - rs, rstr) == 0) { z = t; break; }
+        const Int count = z < 0 ? 0 : Length(n, z, L);
+        if (count > 0) {
+            const size_t es = A.ElemSize();
+            std::vector<unsigned char> host(count * es);
+            const Int step = L / cstr + (L / rstr) * A.LDim();
+            elx::Buffer tmp(A.Dev(), count * es, A.Stream());
+            kern::Copy2D d{count, 1, At(A, (z - cs) / cstr, (z - rs) / rstr), step, 0, tmp.data(), 1, count};
+            exec::Copy2DBatch(A.Dev(), A.Type(), &d, 1, false, 0.0, A.Stream());
+            if (A.Dev() == Device::GPU) {
+                ELX_CHECK_HIP(hipMemcpyAsync(host.data(), tmp.data(), count * es, hipMemcpyDeviceToHost, A.Stream()));
+                ELX_CHECK_HIP(hipStreamSynchronize(A.Stream()));
+            } else {
+                std::memcpy(host.data(), tmp.data(), count * es);
+            }
+            for (Int q = 0; q < count; ++q)
+                if (exec::LoadScalar(A.Type(), host.data() + q * es) == 0.0) zeros += 1;
+        }
+    }
+    return GridAllReduceSum(A.G(), zeros) > 0;
 }
 
 }  // namespace elx

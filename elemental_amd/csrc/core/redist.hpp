@@ -26,4 +26,16 @@ void Combine(int fn, const DistMatrix& A, DistMatrix& B);
 // (same owner of every element): lets SUMMA use views instead of copies.
 bool SameLocalLayout(const DistMatrix& A, Dist cd, Dist rd, int calign, int ralign);
 
+// entry access (El::DistMatrix::Get is collective; Set/Update write the local copies)
+double Get(const DistMatrix& A, Int i, Int j);
+void Set(DistMatrix& A, Int i, Int j, double v);
+void Update(DistMatrix& A, Int i, Int j, double v);
+// El::Fill: every entry := v
+void Fill(DistMatrix& A, double v);
+// collective: is any diagonal entry exactly zero?  (Trsm's checkIfSingular)
+bool DiagonalHasZero(const DistMatrix& A);
+// grid-wide scalar sum / broadcast from VC rank `rootVC`
+double GridAllReduceSum(const Grid& g, double v);
+double GridBcast(const Grid& g, double v, int rootVC);
+
 }  // namespace elx

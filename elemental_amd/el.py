@@ -21,7 +21,7 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
                    VC, VR, call, lib)
 
 __all__ = [
-    "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Hadamard",
+    "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Fill", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
     "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "Symm", "Hemm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
@@ -244,6 +244,20 @@ class DistMatrix:
         call("elx_dm_copy", self.h, other.h)
         return self
 
+    def Get(self, i: int, j: int) -> float:
+        """A.Get(i, j): collective; every rank returns the entry (setup.hpp:463-490)."""
+        v = c_double()
+        call("elx_dm_get", self.h, i, j, byref(v))
+        return v.value
+
+    def Set(self, i: int, j: int, value: float):
+        """A.Set(i, j, value): ranks holding (i, j) write it; not collective."""
+        call("elx_dm_set", self.h, i, j, float(value))
+
+    def Update(self, i: int, j: int, value: float):
+        """A.Update(i, j, value): A(i,j) += value on the ranks holding it."""
+        call("elx_dm_update", self.h, i, j, float(value))
+
     def like(self, U=None, V=None, device=None) -> "DistMatrix":
         U = self.U if U is None else U
         V = self.V if V is None else V
@@ -290,10 +304,11 @@ def Her2k(uplo, orientation, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistM
     Syr2k(uplo, orientation, alpha, A, B, beta, C, conjugate=True)
 
 
-def Trsm(side, uplo, orientation, diag, alpha, A: DistMatrix, B: DistMatrix):
-    """El::Trsm(side, uplo, orientation, diag, alpha, A, B) (Trsm.cpp:129-420): B is
-    overwritten with alpha op(A)^-1 B (LEFT) or alpha B op(A)^-1 (RIGHT)."""
-    call("elx_trsm", side, uplo, orientation, diag, float(alpha), A.h, B.h)
+def Trsm(side, uplo, orientation, diag, alpha, A: DistMatrix, B: DistMatrix, checkIfSingular: bool = False):
+    """El::Trsm(side, uplo, orientation, diag, alpha, A, B, checkIfSingular) (Trsm.cpp:129-420):
+    B is overwritten with alpha op(A)^-1 B (LEFT) or alpha B op(A)^-1 (RIGHT);
+    checkIfSingular raises SingularMatrixError on an exact zero NON_UNIT diagonal."""
+    call("elx_trsm", side, uplo, orientation, diag, float(alpha), A.h, B.h, int(bool(checkIfSingular)))
 
 
 def Symm(side, uplo, alpha, A: DistMatrix, B: DistMatrix, beta, C: DistMatrix, conjugate: bool = False):
@@ -321,6 +336,11 @@ def Scale(alpha, A: DistMatrix):
 
 def Zero(A: DistMatrix):
     call("elx_dm_zero", A.h)
+
+
+def Fill(A: DistMatrix, alpha):
+    """El::Fill(A, alpha) (include/El/blas_like/level1/Fill.hpp:66-70)."""
+    call("elx_dm_fill", A.h, float(alpha))
 
 
 def Hadamard(A, B, C):

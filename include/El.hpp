@@ -10,6 +10,7 @@
 //
 // Link with -lelemental_amd (elemental_amd/libelemental_amd.so).
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -52,6 +53,10 @@ struct UnsupportedError : LogicError { using LogicError::LogicError; };
 namespace hydrogen_errors {
 struct GPUError : std::runtime_error { using std::runtime_error::runtime_error; };  // hydrogen::GPUError
 }
+// include/El/core/environment/decl.hpp:209-214
+struct SingularMatrixException : std::runtime_error {
+    explicit SingularMatrixException(const char* msg = "Matrix was singular") : std::runtime_error(msg) {}
+};
 
 namespace detail {
 inline void Check(int rc) {
@@ -62,6 +67,7 @@ inline void Check(int rc) {
     case ELX_ERR_UNSUPPORTED: throw UnsupportedError(msg);
     case ELX_ERR_HIP:
     case ELX_ERR_NO_DEVICE: throw hydrogen_errors::GPUError(msg);
+    case ELX_ERR_SINGULAR: throw SingularMatrixException(msg.c_str());
     default: throw RuntimeError(msg);
     }
 }
@@ -71,6 +77,47 @@ template <> struct TypeCode<double> { static constexpr int value = ELX_F64; };
 template <> struct TypeCode<gpu_half_type> { static constexpr int value = ELX_F16; };
 template <> struct TypeCode<bfloat16> { static constexpr int value = ELX_BF16; };
 template <typename T> double ToDouble(T x) { return static_cast<double>(x); }
+template <typename T> T FromDouble(double v) { return static_cast<T>(v); }
+// 16-bit values cross the boundary as their exact double widening
+inline double HalfBitsToDouble(std::uint16_t h) {
+    const int e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    const double mag = e == 0 ? std::ldexp(m, -24) : e == 31 ? (m ? NAN : INFINITY) : std::ldexp(1024 + m, e - 25);
+    return (h & 0x8000) ? -mag : mag;
+}
+inline double BF16BitsToDouble(std::uint16_t b) {
+    const std::uint32_t u = static_cast<std::uint32_t>(b) << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+template <> inline double ToDouble(gpu_half_type x) { return HalfBitsToDouble(x.x); }
+template <> inline double ToDouble(bfloat16 x) { return BF16BitsToDouble(x.x); }
+// double -> 16-bit with one round-to-nearest-even (through float is exact for
+// the values Get returns, which are 16-bit already)
+inline std::uint16_t FloatToBF16Bits(float f) {
+    std::uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<std::uint16_t>((u >> 16) | 0x40);
+    return static_cast<std::uint16_t>((u + 0x7fffu + ((u >> 16) & 1)) >> 16);
+}
+inline std::uint16_t FloatToHalfBits(float f) {
+    std::uint32_t u;
+    std::memcpy(&u, &f, 4);
+    const std::uint32_t sign = (u >> 16) & 0x8000u, a = u & 0x7fffffffu;
+    if (a >= 0x7f800000u) return static_cast<std::uint16_t>(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0));
+    if (a >= 0x477ff000u) return static_cast<std::uint16_t>(sign | 0x7c00u);
+    if (a < 0x33000001u) return static_cast<std::uint16_t>(sign);
+    const int e = static_cast<int>(a >> 23);
+    std::uint32_t man = (a & 0x7fffffu) | 0x800000u;
+    const int shift = e < 113 ? 126 - e : 13;
+    std::uint32_t mm = man >> shift;
+    const std::uint32_t rem = man & ((1u << shift) - 1), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (mm & 1))) ++mm;
+    if (e < 113) return static_cast<std::uint16_t>(sign | mm);
+    return static_cast<std::uint16_t>(sign | (((e - 112) << 10) + (mm - 1024)));
+}
+template <> inline gpu_half_type FromDouble(double v) { return gpu_half_type{FloatToHalfBits(static_cast<float>(v))}; }
+template <> inline bfloat16 FromDouble(double v) { return bfloat16{FloatToBF16Bits(static_cast<float>(v))}; }
 }  // namespace detail
 
 // ---- Range / views ---------------------------------------------------------
@@ -96,6 +143,12 @@ public:
     static Comm RCCL(int rank, int size, const unsigned char id[128]) {
         elx_comm_t c = nullptr;
         detail::Check(elx_comm_init_rccl(&c, rank, size, id));
+        return Comm(c);
+    }
+    // a communicator the caller already owns (e.g. LBANN's ncclComm_t); borrowed, not destroyed
+    static Comm FromRCCL(void* ncclComm) {
+        elx_comm_t c = nullptr;
+        detail::Check(elx_comm_wrap_rccl(&c, ncclComm));
         return Comm(c);
     }
     int Rank() const { int r = 0; detail::Check(elx_comm_rank(c_.get(), &r)); return r; }
@@ -132,6 +185,148 @@ private:
     mpi::Comm comm_;
     std::shared_ptr<elx_grid_s> g_;
     int info_[8] = {};
+};
+
+// ---- El::Matrix<T,D> (include/El/core/Matrix/decl.hpp:299-540) -------------------
+// Column-major local matrix on one device: owns its buffer (host memory, or the
+// library's stream-ordered device pool) or views caller storage (Attach /
+// LockedAttach, and the local block a DistMatrix hands out through Matrix()).
+template <typename T>
+class AbstractMatrix {
+public:
+    virtual ~AbstractMatrix() = default;
+    virtual Device GetDevice() const noexcept = 0;
+    virtual void Resize(Int height, Int width) = 0;
+    Int Height() const noexcept { return h_; }
+    Int Width() const noexcept { return w_; }
+    Int LDim() const noexcept { return ld_; }
+    bool Viewing() const noexcept { return !owned_; }
+    bool Locked() const noexcept { return locked_; }
+    T* Buffer() {
+        if (locked_) throw LogicError("Cannot return non-const buffer of locked Matrix");
+        return buf_;
+    }
+    const T* LockedBuffer() const noexcept { return buf_; }
+    T* Buffer(Int i, Int j) { return Buffer() + i + j * ld_; }
+    const T* LockedBuffer(Int i, Int j) const noexcept { return buf_ + i + j * ld_; }
+    // SyncInfoFromMatrix: the HIP stream the matrix's device work is ordered on (null on the CPU)
+    void* Stream() const noexcept { return stream_; }
+
+protected:
+    T* buf_ = nullptr;
+    Int h_ = 0, w_ = 0, ld_ = 1;
+    bool owned_ = true, locked_ = false;
+    void* stream_ = nullptr;
+};
+
+template <typename T, Device D = Device::CPU>
+class Matrix : public AbstractMatrix<T> {
+public:
+    Matrix() { this->stream_ = DefaultStream(); }
+    Matrix(Int height, Int width, Int ldim = 0) : Matrix() { Resize(height, width, ldim); }
+    Matrix(const Matrix& A) : Matrix() { *this = A; }
+    Matrix(Matrix&& A) noexcept { Swap(A); }
+    ~Matrix() { Release(); }
+    Matrix& operator=(const Matrix& A) {  // deep copy (El::Copy of Matrix)
+        if (this == &A) return *this;
+        Resize(A.Height(), A.Width());
+        detail::Check(elx_matrix_copy(detail::TypeCode<T>::value, static_cast<int>(D), A.Height(), A.Width(),
+                                      A.LockedBuffer(), A.LDim(), this->buf_, this->ld_, this->stream_));
+        return *this;
+    }
+    Matrix& operator=(Matrix&& A) noexcept { Swap(A); return *this; }
+    Device GetDevice() const noexcept override { return D; }
+
+    void Resize(Int height, Int width) override { Resize(height, width, height > 1 ? height : 1); }
+    void Resize(Int height, Int width, Int ldim) {
+        if (height < 0 || width < 0) throw LogicError("Height and width must be non-negative");
+        if (ldim <= 0) ldim = height > 1 ? height : 1;
+        if (ldim < height) throw LogicError("Leading dimension must be no less than height");
+        if (!this->owned_) {
+            if (height != this->h_ || width != this->w_) throw LogicError("Cannot resize this matrix");
+            return;
+        }
+        const std::size_t need = static_cast<std::size_t>(ldim) * static_cast<std::size_t>(width);
+        if (need > cap_) {  // grow-only, like Memory::Require (Memory/impl.hpp:254-286)
+            Free();
+            Allocate(need);
+        }
+        this->h_ = height;
+        this->w_ = width;
+        this->ld_ = ldim;
+    }
+    void Empty() { Release(); this->h_ = this->w_ = 0; this->ld_ = 1; }
+    // view caller storage (Matrix::Attach / LockedAttach)
+    void Attach(Int height, Int width, T* buffer, Int ldim) { View(height, width, buffer, ldim, false); }
+    void LockedAttach(Int height, Int width, const T* buffer, Int ldim) {
+        View(height, width, const_cast<T*>(buffer), ldim, true);
+    }
+    // entry access; on the GPU a synchronizing single-element transfer
+    T Get(Int i, Int j) const {
+        CheckIndex(i, j);
+        T v;
+        if (D == Device::GPU)
+            detail::Check(elx_memcpy_d2h(&v, this->buf_ + i + j * this->ld_, sizeof(T), this->stream_));
+        else
+            v = this->buf_[i + j * this->ld_];
+        return v;
+    }
+    void Set(Int i, Int j, T v) {
+        CheckIndex(i, j);
+        T* p = this->Buffer() + i + j * this->ld_;
+        if (D == Device::GPU) detail::Check(elx_memcpy_h2d(p, &v, sizeof(T), this->stream_));
+        else *p = v;
+    }
+    // SetSyncInfo(Matrix, SyncInfo): subsequent device work queues on `stream`
+    void SetStream(void* stream) { if (D == Device::GPU) this->stream_ = stream ? stream : DefaultStream(); }
+
+private:
+    static void* DefaultStream() {
+        if (D != Device::GPU) return nullptr;
+        void* s = nullptr;
+        detail::Check(elx_default_stream(&s));
+        return s;
+    }
+    void CheckIndex(Int i, Int j) const {
+        if (i < 0 || j < 0 || i >= this->h_ || j >= this->w_) throw LogicError("Entry out of bounds");
+    }
+    void View(Int height, Int width, T* buffer, Int ldim, bool locked) {
+        if (ldim < (height > 1 ? height : 1)) throw LogicError("Leading dimension must be no less than height");
+        Release();
+        this->buf_ = buffer;
+        this->h_ = height;
+        this->w_ = width;
+        this->ld_ = ldim;
+        this->owned_ = false;
+        this->locked_ = locked;
+    }
+    void Allocate(std::size_t elems) {
+        void* p = nullptr;
+        if (elems) {
+            if (D == Device::GPU) {
+                detail::Check(elx_pool_alloc(&p, elems * sizeof(T), this->stream_));
+            } else {
+                p = ::operator new(elems * sizeof(T));
+            }
+        }
+        this->buf_ = static_cast<T*>(p);
+        cap_ = elems;
+    }
+    void Free() {
+        if (this->owned_ && this->buf_) {
+            if (D == Device::GPU) (void)elx_pool_free(this->buf_, this->stream_);
+            else ::operator delete(this->buf_);
+        }
+        this->buf_ = nullptr;
+        cap_ = 0;
+    }
+    void Release() { Free(); this->owned_ = true; this->locked_ = false; }
+    void Swap(Matrix& o) noexcept {
+        std::swap(this->buf_, o.buf_); std::swap(this->h_, o.h_); std::swap(this->w_, o.w_);
+        std::swap(this->ld_, o.ld_); std::swap(this->owned_, o.owned_); std::swap(this->locked_, o.locked_);
+        std::swap(this->stream_, o.stream_); std::swap(cap_, o.cap_);
+    }
+    std::size_t cap_ = 0;
 };
 
 // ---- DistMatrix ----------------------------------------------------------------
@@ -177,6 +372,15 @@ public:
     void SetLocalBlock(const T* host, Int ld) { detail::Check(elx_dm_set_local(h(), host, ld)); }
     void GetLocalBlock(T* host, Int ld) const { detail::Check(elx_dm_get_local(h(), host, ld)); }
     void Synchronize() const { detail::Check(elx_dm_synchronize(h())); }
+    // entry access (ElementMatrix/setup.hpp:463-610): Get is collective over the
+    // grid; Set / Update write the copies held by this rank
+    T Get(Int i, Int j) const {
+        double v = 0;
+        detail::Check(elx_dm_get(h(), i, j, &v));
+        return detail::FromDouble<T>(v);
+    }
+    void Set(Int i, Int j, T value) { detail::Check(elx_dm_set(h(), i, j, detail::ToDouble(value))); }
+    void Update(Int i, Int j, T value) { detail::Check(elx_dm_update(h(), i, j, detail::ToDouble(value))); }
     // SetSyncInfo(mat, si) / SyncInfoFromMatrix(mat): the matrix's HIP stream
     void SetStream(void* stream) { detail::Check(elx_dm_set_stream(h(), stream)); }
     void* Stream() const { void* s = nullptr; detail::Check(elx_dm_stream(h(), &s)); return s; }
@@ -224,12 +428,23 @@ public:
         detail::Check(elx_dm_copy(this->h(), A.h()));
         return *this;
     }
+    // the local block as an El::Matrix<T,D> view (ElementalMatrix::Matrix() /
+    // LockedMatrix(), include/El/core/DistMatrix/Element.hpp): buffer, local
+    // sizes, ldim and the matrix's stream, refreshed on every call
+    El::Matrix<T, D>& Matrix() { RefreshLocal(); return local_; }
+    const El::Matrix<T, D>& LockedMatrix() const { RefreshLocal(); return local_; }
     // A(IR(i0,i1), IR(j0,j1)) views
     DistMatrix operator()(Range rows, Range cols) const { return View(rows.beg, rows.end, cols.beg, cols.end); }
     DistMatrix operator()(AllRange, Range cols) const { return View(0, this->Height(), cols.beg, cols.end); }
     DistMatrix operator()(Range rows, AllRange) const { return View(rows.beg, rows.end, 0, this->Width()); }
 
 private:
+    void RefreshLocal() const {
+        const Int ld = this->LDim() > 1 ? this->LDim() : 1;
+        local_.Attach(this->LocalHeight(), this->LocalWidth(), const_cast<T*>(this->LockedBuffer()), ld);
+        local_.SetStream(this->Stream());
+    }
+    mutable El::Matrix<T, D> local_;
     DistMatrix(const El::Grid& g, elx_dm_t view) : AbstractDistMatrix<T>(g, U, V, D, view) {}
     DistMatrix View(Int i0, Int i1, Int j0, Int j1) const {
         elx_dm_t v = nullptr;
@@ -239,6 +454,39 @@ private:
 };
 
 // ---- level 3 (include/El/blas_like/level3.hpp:37-90) ----------------------------
+// Gemm on local matrices (level3.hpp:37-65, Gemm.cpp:141-250): the MFMA kernels on
+// the GPU (on C's stream), the library's host loops on the CPU
+template <typename T>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractMatrix<T>& A, const AbstractMatrix<T>& B,
+          T beta, AbstractMatrix<T>& C) {
+    if (A.GetDevice() != C.GetDevice() || B.GetDevice() != C.GetDevice())
+        throw LogicError("Gemm: A, B and C must be on the same device");
+    const Int m = orientA == NORMAL ? A.Height() : A.Width(), k = orientA == NORMAL ? A.Width() : A.Height();
+    const Int kb = orientB == NORMAL ? B.Height() : B.Width(), n = orientB == NORMAL ? B.Width() : B.Height();
+    if (m != C.Height() || n != C.Width() || k != kb) throw LogicError("Nonconformal Gemm");
+    detail::Check(elx_matrix_gemm(detail::TypeCode<T>::value, static_cast<int>(C.GetDevice()), orientA, orientB, m, n,
+                                  k, detail::ToDouble(alpha), A.LockedBuffer(), A.LDim(), B.LockedBuffer(), B.LDim(),
+                                  detail::ToDouble(beta), C.Buffer(), C.LDim(), C.Stream()));
+}
+// beta-less form: C resized to op(A) op(B) and overwritten
+template <typename T>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractMatrix<T>& A, const AbstractMatrix<T>& B,
+          AbstractMatrix<T>& C) {
+    C.Resize(orientA == NORMAL ? A.Height() : A.Width(), orientB == NORMAL ? B.Width() : B.Height());
+    Gemm(orientA, orientB, alpha, A, B, detail::FromDouble<T>(0.0), C);
+}
+template <typename T, Device D>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const Matrix<T, D>& A, const Matrix<T, D>& B, T beta,
+          Matrix<T, D>& C) {
+    Gemm(orientA, orientB, alpha, static_cast<const AbstractMatrix<T>&>(A), static_cast<const AbstractMatrix<T>&>(B),
+         beta, static_cast<AbstractMatrix<T>&>(C));
+}
+template <typename T, Device D>
+void Gemm(Orientation orientA, Orientation orientB, T alpha, const Matrix<T, D>& A, const Matrix<T, D>& B,
+          Matrix<T, D>& C) {
+    Gemm(orientA, orientB, alpha, static_cast<const AbstractMatrix<T>&>(A), static_cast<const AbstractMatrix<T>&>(B),
+         static_cast<AbstractMatrix<T>&>(C));
+}
 template <typename T>
 void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractDistMatrix<T>& A,
           const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C, GemmAlgorithm alg = GEMM_DEFAULT) {
@@ -294,10 +542,12 @@ void Her2k(UpperOrLower uplo, Orientation orientation, T alpha, const AbstractDi
            const AbstractDistMatrix<T>& B, T beta, AbstractDistMatrix<T>& C) {
     Syr2k(uplo, orientation, alpha, A, B, beta, C, true);
 }
+// checkIfSingular: SingularMatrixException on an exact zero NON_UNIT diagonal (Trsm.cpp:60-68)
 template <typename T>
 void Trsm(LeftOrRight side, UpperOrLower uplo, Orientation orientation, UnitOrNonUnit diag, T alpha,
-          const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) {
-    detail::Check(elx_trsm(side, uplo, orientation, diag, detail::ToDouble(alpha), A.h(), B.h()));
+          const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B, bool checkIfSingular = false) {
+    detail::Check(elx_trsm(side, uplo, orientation, diag, detail::ToDouble(alpha), A.h(), B.h(),
+                           checkIfSingular ? 1 : 0));
 }
 template <typename T>
 void Symm(LeftOrRight side, UpperOrLower uplo, T alpha, const AbstractDistMatrix<T>& A, const AbstractDistMatrix<T>& B,
@@ -328,6 +578,33 @@ template <typename T, typename S> void Scale(S alpha, AbstractDistMatrix<T>& A) 
     detail::Check(elx_dm_scale(static_cast<double>(alpha), A.h()));
 }
 template <typename T> void Zero(AbstractDistMatrix<T>& A) { detail::Check(elx_dm_zero(A.h())); }
+// El::Fill (include/El/blas_like/level1/Fill.hpp:20-70)
+template <typename T> void Fill(AbstractDistMatrix<T>& A, T alpha) {
+    detail::Check(elx_dm_fill(A.h(), detail::ToDouble(alpha)));
+}
+// level-1 on local matrices (Fill / Zero / Scale / Axpy / Copy of AbstractMatrix)
+template <typename T> void Fill(AbstractMatrix<T>& A, T alpha) {
+    detail::Check(elx_matrix_fill(detail::TypeCode<T>::value, static_cast<int>(A.GetDevice()), A.Height(), A.Width(),
+                                  detail::ToDouble(alpha), A.Buffer(), A.LDim(), A.Stream()));
+}
+template <typename T> void Zero(AbstractMatrix<T>& A) { Fill(A, detail::FromDouble<T>(0.0)); }
+template <typename T, typename S> void Scale(S alpha, AbstractMatrix<T>& A) {
+    detail::Check(elx_matrix_scale(detail::TypeCode<T>::value, static_cast<int>(A.GetDevice()), A.Height(), A.Width(),
+                                   static_cast<double>(alpha), A.Buffer(), A.LDim(), A.Stream()));
+}
+template <typename T, typename S> void Axpy(S alpha, const AbstractMatrix<T>& X, AbstractMatrix<T>& Y) {
+    if (X.GetDevice() != Y.GetDevice()) throw LogicError("Axpy: X and Y must be on the same device");
+    if (X.Height() != Y.Height() || X.Width() != Y.Width()) throw LogicError("Nonconformal Axpy");
+    detail::Check(elx_matrix_axpy(detail::TypeCode<T>::value, static_cast<int>(Y.GetDevice()), Y.Height(), Y.Width(),
+                                  static_cast<double>(alpha), X.LockedBuffer(), X.LDim(), Y.Buffer(), Y.LDim(),
+                                  Y.Stream()));
+}
+template <typename T> void Copy(const AbstractMatrix<T>& A, AbstractMatrix<T>& B) {
+    if (A.GetDevice() != B.GetDevice()) throw LogicError("Copy: cross-device Matrix copies go through DistMatrix");
+    B.Resize(A.Height(), A.Width());
+    detail::Check(elx_matrix_copy(detail::TypeCode<T>::value, static_cast<int>(B.GetDevice()), A.Height(), A.Width(),
+                                  A.LockedBuffer(), A.LDim(), B.Buffer(), B.LDim(), B.Stream()));
+}
 template <typename T> void Hadamard(const AbstractDistMatrix<T>& A, const AbstractDistMatrix<T>& B, AbstractDistMatrix<T>& C) {
     detail::Check(elx_dm_hadamard(A.h(), B.h(), C.h()));
 }

@@ -28,6 +28,7 @@ extern "C" {
 #define ELX_ERR_RUNTIME         4  /* El::RuntimeError                           */
 #define ELX_ERR_UNSUPPORTED     5  /* "Bad device/type combo" LogicErrors        */
 #define ELX_ERR_NO_DEVICE       6  /* no gfx950 device visible                   */
+#define ELX_ERR_SINGULAR        7  /* El::SingularMatrixException                */
 
 /* ---- enums: ordinals match the reference ------------------------------- */
 /* El::Orientation  include/El/core/types.hpp:463-469 */
@@ -140,6 +141,24 @@ int elx_gemm_bf16(int opA, int opB, int64_t m, int64_t n, int64_t k,
                   const uint16_t* B, int64_t ldb,
                   float beta, uint16_t* C, int64_t ldc, void* stream);
 
+/* ---- El::Matrix<T,D> on either device (device = ELX_DEVICE_*; stream ignored on
+ * the CPU).  gemm replaces Gemm(Orientation, Orientation, T, Matrix<T,D> const&,
+ * Matrix<T,D> const&, T, Matrix<T,D>&) (include/El/blas_like/level3.hpp:37-65,
+ * src/blas_like/level3/Gemm.cpp:141-250; k == 0 -> C := beta C); fill / scale /
+ * axpy / copy replace El::Fill / Scale / Axpy / Copy on Matrix<T,D>
+ * (include/El/blas_like/level1/{Fill,Scale,Axpy,Copy}.hpp). */
+int elx_matrix_gemm(int dtype, int device, int opA, int opB, int64_t m, int64_t n, int64_t k,
+                    double alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
+                    double beta, void* C, int64_t ldc, void* stream);
+int elx_matrix_fill(int dtype, int device, int64_t m, int64_t n, double value,
+                    void* A, int64_t lda, void* stream);
+int elx_matrix_scale(int dtype, int device, int64_t m, int64_t n, double alpha,
+                     void* A, int64_t lda, void* stream);
+int elx_matrix_axpy(int dtype, int device, int64_t m, int64_t n, double alpha,
+                    const void* X, int64_t ldx, void* Y, int64_t ldy, void* stream);
+int elx_matrix_copy(int dtype, int device, int64_t m, int64_t n, const void* A, int64_t lda,
+                    void* B, int64_t ldb, void* stream);
+
 /* ---- BLAS-1 entrywise kernels (dtype-generic; scalars passed as double) --
  * Strides are element strides: X(i,j) = X[i*xcs + j*xrs].
  * axpy2d   replaces Axpy_GPU_impl            (src/hydrogen/blas/gpu/Axpy.cu:119-189)
@@ -205,6 +224,10 @@ int elx_comm_unique_id(unsigned char id[128]);
 int elx_comm_init_rccl(elx_comm_t* world, int rank, int size, const unsigned char id[128]);
 int elx_comm_init_host(elx_comm_t* world, int rank, int size,
                        elx_host_coll_fn coll, elx_host_split_fn split, void* ctx);
+/* Grid(mpi::Comm) from a communicator the caller already owns: borrow an
+ * existing RCCL communicator (ncclComm_t passed as void*; never destroyed by
+ * the library, its grid splits are) */
+int elx_comm_wrap_rccl(elx_comm_t* comm, void* nccl_comm);
 int elx_comm_rank(elx_comm_t comm, int* rank);
 int elx_comm_size(elx_comm_t comm, int* size);
 int elx_comm_destroy(elx_comm_t comm);
@@ -285,6 +308,15 @@ int elx_dm_read(elx_dm_t A, const char* filename, int format, int int_bytes);
 int elx_dm_set_stream(elx_dm_t A, void* stream);
 int elx_dm_stream(elx_dm_t A, void** stream);
 
+/* DistMatrix::Get (ElementMatrix/setup.hpp:463-490): collective over the grid,
+ * every rank returns A(i,j) (16-bit values widened exactly to double).
+ * Set / Update (setup.hpp:552-604): each rank holding (i,j) writes its copy;
+ * not collective.  Fill (Fill.hpp:20-70): every entry := value. */
+int elx_dm_get(elx_dm_t A, int64_t i, int64_t j, double* value);
+int elx_dm_set(elx_dm_t A, int64_t i, int64_t j, double value);
+int elx_dm_update(elx_dm_t A, int64_t i, int64_t j, double value);
+int elx_dm_fill(elx_dm_t A, double value);
+
 /* ---- distributed BLAS-1 front doors (include/El/blas_like/level1/) ---- */
 int elx_dm_axpy(double alpha, elx_dm_t X, elx_dm_t Y);       /* Axpy.hpp:151-176     */
 int elx_dm_scale(double alpha, elx_dm_t A);                   /* Scale.hpp:18-31      */
@@ -315,7 +347,8 @@ int elx_syr2k(int uplo, int orient, double alpha, elx_dm_t A, elx_dm_t B, double
               elx_dm_t C, int conjugate);
 /* El::Trsm on DistMatrices (src/blas_like/level3/Trsm.cpp:129-420): B := alpha
  * op(A)^-1 B (ELX_LEFT) or alpha B op(A)^-1 (ELX_RIGHT); float and double */
-int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B);
+int elx_trsm(int side, int uplo, int orient, int diag, double alpha, elx_dm_t A, elx_dm_t B,
+             int checkIfSingular);  /* ELX_ERR_SINGULAR on an exact zero NON_UNIT diagonal (Trsm.cpp:60-68) */
 /* El::Symm / El::Hemm (src/blas_like/level3/Symm.cpp:55-80): C := alpha A B + beta C
  * (ELX_LEFT) or alpha B A + beta C (ELX_RIGHT); A symmetric, only its uplo triangle read */
 int elx_symm(int side, int uplo, double alpha, elx_dm_t A, elx_dm_t B, double beta, elx_dm_t C,
@@ -337,6 +370,12 @@ int elx_last_gemm_algorithm(void);
 int elx_set_profiling(int on);
 int elx_profile_stats(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops,
                       double* comm_ms, int64_t* comm_bytes);
+/* transfer-only timing of the RCCL exchanges (events around each grouped
+ * send/recv on its stream, pack/unpack excluded): summed ms, bytes received */
+int elx_profile_transfers(double* transfer_ms, int64_t* bytes, int64_t* transfers);
+/* compute-stream idle time between consecutive SUMMA panel updates (what the
+ * panel pipeline failed to hide), summed over the profiled calls */
+int elx_profile_pipeline(double* gap_ms, int64_t* gaps);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ import traceback
 import numpy as np
 
 ORIENTS = {0: "N", 1: "T", 2: "T"}
+W_FMT = {0: "f32", 1: "f64", 2: "f16", 3: "bf16"}  # ELX_F32, ELX_F64, ELX_F16, ELX_BF16
 
 
 def init(rank: int, world: int, port: int):
@@ -89,27 +90,44 @@ def redist_worker(rank: int, world: int, port: int, height: int, device: int, dt
 
 
 def _tol(dtype):
-    return {0: np.finfo(np.float32).eps, 1: np.finfo(np.float64).eps}[dtype]
+    """Unit roundoff the normwise bound uses: f32/f64 eps; for the 16-bit types
+    the storage format's (2^-11 f16, 2^-8 bf16) against the exact product of the
+    16-bit inputs, as test_local_gemm_16bit."""
+    return {0: np.finfo(np.float32).eps, 1: np.finfo(np.float64).eps, 2: 2.0 ** -11, 3: 2.0 ** -8}[dtype]
+
+
+def _host_dt(dtype):
+    return {0: np.float32, 1: np.float64, 2: np.float16, 3: "bf16"}[dtype]
 
 
 def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, algs,
-                nb: int, seed: int):
+                nb: int, seed: int, kc: int = 0):
+    """El::Gemm NN/NT/TN/TT x `algs` against the oracle (north_star normwise
+    tolerance).  kc > 0 forces the C-stationary compute panel to kc columns, so
+    k >= 2 kc runs several panels through the two-slot pipeline: on grids larger
+    than 1x1 every slot is refilled (gathered) while the previous update may still
+    read it (the write-after-read fence of NN.hpp:371-384's loop)."""
     import oracle
     el, comm = init(rank, world, port)
     try:
         g = el.Grid(comm, height)
         r, c = g.height, g.width
-        npdt = np.float64 if dtype == el.F64 else np.float32
+        fmt = W_FMT[dtype]
+        npdt = _host_dt(dtype)
         el.SetBlocksize(nb)
-        el.SetComputePanel(0)
+        el.SetComputePanel(kc)
         for (m, n, k) in shapes:
             for oA in (el.NORMAL, el.TRANSPOSE):
                 for oB in (el.NORMAL, el.TRANSPOSE):
                     Ag = oracle.hash_matrix(m if oA == 0 else k, k if oA == 0 else m, seed + 1, -0.1, 0.1, npdt)
                     Bg = oracle.hash_matrix(k if oB == 0 else n, n if oB == 0 else k, seed + 2, -0.1, 0.1, npdt)
                     Cg = oracle.hash_matrix(m, n, seed + 3, -0.1, 0.1, npdt)
+                    Af, Bf, Cf = (oracle.to_f64(x, fmt) for x in (Ag, Bg, Cg))
                     alpha, beta = 0.5, -0.5  # Gemm_Suite.cpp:158-172
-                    ref = oracle.gemm(ORIENTS[oA], ORIENTS[oB], alpha, Ag, Bg, beta, Cg)
+                    # f64/f32: the reference's loop nest in the working precision;
+                    # 16-bit: the exact product of the 16-bit inputs
+                    ref = oracle.gemm(ORIENTS[oA], ORIENTS[oB], alpha, Ag, Bg, beta, Cg) if dtype in (0, 1) else \
+                        oracle.gemm(ORIENTS[oA], ORIENTS[oB], alpha, Af, Bf, beta, Cf)
                     for alg in algs:
                         A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Ag.shape[0], width=Ag.shape[1])
                         B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=Bg.shape[0], width=Bg.shape[1])
@@ -118,14 +136,15 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
                         B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
                         C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
                         ran = el.Gemm(oA, oB, alpha, A, B, beta, C, alg)
-                        got = C.get_local().astype(np.float64)
+                        got = oracle.to_f64(C.get_local(), fmt)
                         want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
                         # north_star normwise bound, applied blockwise with the global norms
                         num = np.linalg.norm(got - want) if got.size else 0.0
-                        den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) \
-                            * max(k, 1) * _tol(dtype)
-                        assert num <= 10 * den, (f"Gemm {ORIENTS[oA]}{ORIENTS[oB]} alg {alg}->{ran} "
-                                                 f"{m}x{n}x{k} grid {r}x{c} rank {rank}: {num / den:.3g}")
+                        den = np.linalg.norm(Af) * np.linalg.norm(Bf) * max(k, 1) * _tol(dtype)
+                        assert np.isfinite(got).all() and num <= 10 * den, (
+                            f"Gemm {fmt} {ORIENTS[oA]}{ORIENTS[oB]} alg {alg}->{ran} {m}x{n}x{k} kc {kc} "
+                            f"grid {r}x{c} rank {rank}: {num / den:.3g}")
+        el.SetComputePanel(0)
         finish()
     except Exception:
         traceback.print_exc()
@@ -133,7 +152,7 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
 
 
 def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, nb: int,
-                seed: int):
+                seed: int, kc: int = 0):
     """El::Syrk/Herk, Syr2k/Her2k and Trrk, LOWER/UPPER x NORMAL/TRANSPOSE
     (Syrk/*.hpp, Syr2k/*.hpp, Trrk/*.hpp): the uplo triangle against the oracle
     (north_star tolerance), the other triangle bit-identical to the input
@@ -145,6 +164,7 @@ def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         r, c = g.height, g.width
         npdt = np.float64 if dtype == el.F64 else np.float32
         el.SetBlocksize(nb)
+        el.SetComputePanel(kc)  # kc > 0: several panels through the triangular pipeline
         for (n, k) in shapes:
             for uplo in (el.LOWER, el.UPPER):
                 for orient in (el.NORMAL, el.TRANSPOSE):
@@ -208,6 +228,7 @@ def syrk_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
                     den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Tg.astype(np.float64)) \
                         * max(k, 1) * _tol(dtype)
                     assert num <= 10 * den, f"Trrk uplo {uplo} oA {orient} oB {oB} rank {rank}: {num / den:.3g}"
+        el.SetComputePanel(0)
         finish()
     except Exception:
         traceback.print_exc()
@@ -445,6 +466,38 @@ def blas1_worker(rank: int, world: int, port: int, height: int, device: int, see
             raise AssertionError("Combine across distributions must raise")
         except el.L.LogicError:
             pass
+        # C5's entrywise half: 16-bit Axpy / Hadamard on [MC,MR] (every operation in
+        # f32, rounded once to the storage format), plus the in-place Hadamard
+        # forms (Z aliasing X or Y, Hadamard.cu:64-116), bit-exact
+        for dt, fmt in ((el.F16, "f16"), (el.BF16, "bf16")):
+            npdt = _host_dt(dt)
+            X16 = oracle.hash_matrix(m, n, seed + 5, 0.0, 4.0, npdt)
+            Y16 = oracle.hash_matrix(m, n, seed + 6, 0.0, 4.0, npdt)
+            xf, yf = oracle.to_f64(X16, fmt), oracle.to_f64(Y16, fmt)
+
+            def stored(v):  # f32 result -> the 16-bit storage array
+                return oracle.convert(np.asarray(v, np.float32).astype(np.float64), "f64", fmt)
+
+            Xd = el.DistMatrix(g, dt, el.MC, el.MR, device, height=m, width=n)
+            Yd = el.DistMatrix(g, dt, el.MC, el.MR, device, height=m, width=n)
+            Xd.set_local(oracle.local_block(X16, el.MC, el.MR, r, c, g.vc_rank))
+            Yd.set_local(oracle.local_block(Y16, el.MC, el.MR, r, c, g.vc_rank))
+            el.Axpy(2.0, Xd, Yd)
+            want = stored(yf.astype(np.float32) + np.float32(2.0) * xf.astype(np.float32))
+            assert np.array_equal(_bits(Yd.get_local()), _bits(oracle.local_block(want, el.MC, el.MR, r, c,
+                                                                                  g.vc_rank))), f"Axpy {fmt}"
+            Zd = el.DistMatrix(g, dt, el.MC, el.MR, device)
+            el.Hadamard(Xd, Yd, Zd)
+            y2 = oracle.to_f64(want, fmt)
+            prod = stored(xf.astype(np.float32) * y2.astype(np.float32))
+            assert np.array_equal(_bits(Zd.get_local()), _bits(oracle.local_block(prod, el.MC, el.MR, r, c,
+                                                                                  g.vc_rank))), f"Hadamard {fmt}"
+            el.Hadamard(Xd, Yd, Yd)  # Y := X .* Y in place (C aliases B)
+            assert np.array_equal(_bits(Yd.get_local()), _bits(Zd.get_local())), f"in-place Hadamard (C = B) {fmt}"
+            el.Hadamard(Xd, Xd, Xd)  # X := X .* X in place (C aliases A and B)
+            sq = stored(xf.astype(np.float32) * xf.astype(np.float32))
+            assert np.array_equal(_bits(Xd.get_local()), _bits(oracle.local_block(sq, el.MC, el.MR, r, c,
+                                                                                  g.vc_rank))), f"X.*X in place {fmt}"
         finish()
     except Exception:
         traceback.print_exc()
@@ -562,6 +615,106 @@ def convert_worker(rank: int, world: int, port: int, height: int, device: int, s
                               f"[{el.DIST_NAMES[U]},{el.DIST_NAMES[V]}] grid {r}x{c} rank {rank}"
                         assert got.shape == want.shape, f"{tag}: shape {got.shape} vs {want.shape}"
                         assert np.array_equal(_bits(got), _bits(want)), f"{tag}: data mismatch"
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def xdevice_worker(rank: int, world: int, port: int, height: int, seed: int):
+    """Cross-device DistMatrix copies (ElementMatrix/setup.hpp:80-160, the CPU<->GPU
+    copy constructors BasicGemm.cpp:96-234 validates with), both directions, into
+    other distributions and alignments, bit-exact; then Level-3 calls on
+    mixed-device operands (A, B brought to C's / X's device like
+    DistMatrixReadProxy, Gemm/NN.hpp:357-359) against the oracle."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        m, n = 17, 13
+        G = oracle.hash_matrix(m, n, seed, 0.0, 3.0)
+        pairs = [((el.MC, el.MR), (el.MC, el.MR)), ((el.MC, el.MR), (el.STAR, el.VR)),
+                 ((el.VC, el.STAR), (el.MR, el.MC)), ((el.STAR, el.STAR), (el.MC, el.STAR)),
+                 ((el.CIRC, el.CIRC), (el.VR, el.STAR))]
+        for src_dev, dst_dev in ((el.CPU, el.GPU), (el.GPU, el.CPU)):
+            for (U, V), (X, Y) in pairs:
+                A = el.DistMatrix(g, el.F64, U, V, src_dev)
+                A.Align(1 % oracle.lib().orc_dist_stride(U, r, c), 0)
+                A.Resize(m, n)
+                A.set_local(oracle.local_block(G, U, V, r, c, g.vc_rank, A.ColAlign(), A.RowAlign(), 0))
+                for xa in range(min(2, oracle.lib().orc_dist_stride(X, r, c))):
+                    B = el.DistMatrix(g, el.F64, X, Y, dst_dev).Align(xa, 0)
+                    B.assign(A)
+                    want = oracle.local_block(G, X, Y, r, c, g.vc_rank, xa, 0, 0)
+                    assert np.array_equal(_bits(B.get_local()), _bits(want)), \
+                        (src_dev, dst_dev, el.DIST_NAMES[U], el.DIST_NAMES[V], el.DIST_NAMES[X], el.DIST_NAMES[Y])
+        # El::Gemm with A on one device and B, C on another (both ways)
+        mm, nn, kk = 19, 11, 23
+        Ag = oracle.hash_matrix(mm, kk, seed + 1, -0.1, 0.1)
+        Bg = oracle.hash_matrix(kk, nn, seed + 2, -0.1, 0.1)
+        Cg = oracle.hash_matrix(mm, nn, seed + 3, -0.1, 0.1)
+        ref = oracle.gemm("N", "N", 0.5, Ag, Bg, -0.5, Cg)
+        for a_dev, c_dev in ((el.CPU, el.GPU), (el.GPU, el.CPU)):
+            for alg in (el.GEMM_SUMMA_C, el.GEMM_SUMMA_A, el.GEMM_SUMMA_DOT):
+                A = el.DistMatrix(g, el.F64, el.MC, el.MR, a_dev, height=mm, width=kk)
+                B = el.DistMatrix(g, el.F64, el.VC, el.STAR, c_dev, height=kk, width=nn)
+                C = el.DistMatrix(g, el.F64, el.MC, el.MR, c_dev, height=mm, width=nn)
+                A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+                B.set_local(oracle.local_block(Bg, el.VC, el.STAR, r, c, g.vc_rank))
+                C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, alg)
+                got = C.get_local()
+                want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank)
+                num = np.linalg.norm(got - want) if got.size else 0.0
+                den = np.linalg.norm(Ag) * np.linalg.norm(Bg) * kk * _tol(1)
+                assert num <= 10 * den, (a_dev, c_dev, alg, num / den)
+        # El::Trsm with the triangle on the CPU and the right-hand sides on the GPU
+        Tg = oracle.hash_matrix(kk, kk, seed + 4, 0.0, 0.3)
+        Tg[np.diag_indices(kk)] += 2.0
+        Rg = oracle.hash_matrix(kk, nn, seed + 5, -1.0, 1.0)
+        T = el.DistMatrix(g, el.F64, el.MC, el.MR, el.CPU, height=kk, width=kk)
+        R = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=kk, width=nn)
+        T.set_local(oracle.local_block(Tg, el.MC, el.MR, r, c, g.vc_rank))
+        R.set_local(oracle.local_block(Rg, el.MC, el.MR, r, c, g.vc_rank))
+        el.Trsm(el.LEFT, el.LOWER, el.NORMAL, el.NON_UNIT, 1.0, T, R)
+        ref = oracle.trsm("L", "L", "N", "N", 1.0, Tg, Rg)
+        got = R.get_local()
+        want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank)
+        assert np.linalg.norm(got - want) <= 10 * np.linalg.norm(ref) * kk * _tol(1)
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def half_sum_worker(rank: int, world: int, port: int, seed: int):
+    """elx_comm_reduce_scatter / allreduce in f16 and bf16 over the host
+    backend against the rank-order fold with per-addition 16-bit rounding."""
+    import ctypes
+    import oracle
+    from elemental_amd import _lib as L
+    el, comm = init(rank, world, port)
+    try:
+        count = 37
+        for dt, fmt in ((el.F16, "f16"), (el.BF16, "bf16")):
+            npdt = _host_dt(dt)
+            contrib = [oracle.hash_matrix(count * world, 1, seed + q, 0.0, 8.0, npdt).ravel(order="F")
+                       for q in range(world)]
+            send = np.ascontiguousarray(contrib[rank])
+            recv = np.zeros(count, dtype=send.dtype)
+            L.call("elx_comm_reduce_scatter", comm.h, dt, send.ctypes.data_as(ctypes.c_void_p),
+                   recv.ctypes.data_as(ctypes.c_void_p), count, None)
+
+            def fold(parts):
+                acc = oracle.to_f64(parts[0], fmt)
+                for q in range(1, len(parts)):
+                    s32 = (oracle.to_f64(parts[q], fmt).astype(np.float32) + acc.astype(np.float32))
+                    acc = oracle.round_to_format(s32.astype(np.float64), fmt)
+                return acc
+
+            want = fold([c[rank * count:(rank + 1) * count] for c in contrib])
+            assert np.array_equal(oracle.to_f64(recv, fmt), want), (fmt, rank)
         finish()
     except Exception:
         traceback.print_exc()

@@ -1,7 +1,8 @@
-// Compiled check of the drop-in C++ surface (include/El.hpp) on Device::CPU
-// matrices over a 1x1 grid: it must compile the way reference callers write
-// El::Gemm code (tests/blas_like/Gemm.cpp:20-140 shape) and give the same
-// answers as a plain triple loop.  Built and run by tests/test_capi_cpu.py.
+// Compiled check of the drop-in C++ surface (include/El.hpp) over a 1x1 grid:
+// it must compile the way reference callers write El::Gemm code
+// (tests/blas_like/Gemm.cpp:20-140 shape) and give the same answers as a plain
+// triple loop.  Built and run on Device::CPU matrices by tests/test_capi_cpu.py
+// and, with -DEL_TEST_GPU, on Device::GPU matrices by tests/test_gpu_dist.py.
 #include <El.hpp>
 #include <unistd.h>
 #include <cstdio>
@@ -10,6 +11,14 @@
 #include <cmath>
 #include <cstdio>
 #include <vector>
+
+#ifdef EL_TEST_GPU
+constexpr El::Device kDev = El::Device::GPU;
+#else
+constexpr El::Device kDev = El::Device::CPU;
+#endif
+template <typename T, El::Dist U = El::MC, El::Dist V = El::MR>
+using DM = El::DistMatrix<T, U, V, El::ELEMENT, kDev>;
 
 static int failures = 0;
 #define EXPECT(cond)                                                        \
@@ -21,9 +30,18 @@ static int failures = 0;
     } while (0)
 
 template <typename T, El::Dist U, El::Dist V>
-static std::vector<T> Local(const El::DistMatrix<T, U, V>& A) {
+static std::vector<T> Local(const DM<T, U, V>& A) {
     std::vector<T> h(std::max<El::Int>(A.LocalHeight() * A.LocalWidth(), 1));
     A.GetLocalBlock(h.data(), std::max<El::Int>(A.LocalHeight(), 1));
+    return h;
+}
+
+// host copy of a local matrix (entry by entry: small test sizes only)
+template <typename T>
+static std::vector<T> HostOf(const El::Matrix<T, kDev>& M) {
+    std::vector<T> h(M.LDim() * M.Width());
+    for (El::Int j = 0; j < M.Width(); ++j)
+        for (El::Int i = 0; i < M.Height(); ++i) h[i + j * M.LDim()] = M.Get(i, j);
     return h;
 }
 
@@ -35,12 +53,12 @@ int main() {
     EXPECT(El::Grid::DefaultHeight(8) == 2 && El::Grid::DefaultHeight(4) == 2 && El::Grid::DefaultHeight(2) == 1);
 
     const Int m = 37, n = 29, k = 41;
-    El::DistMatrix<double> A(m, k, g), B(k, n, g), C(m, n, g);
+    DM<double> A(m, k, g), B(k, n, g), C(m, n, g);
     El::HashFill(A, 11, 0.0, 1.0);
     El::HashFill(B, 12, 0.0, 1.0);
     El::HashFill(C, 13, 0.0, 1.0);
     EXPECT(A.Height() == m && A.Width() == k && A.LocalHeight() == m && A.LDim() >= m);
-    EXPECT(A.ColDist() == El::MC && A.RowDist() == El::MR && A.GetLocalDevice() == El::Device::CPU);
+    EXPECT(A.ColDist() == El::MC && A.RowDist() == El::MR && A.GetLocalDevice() == kDev);
     const auto a = Local(A), b = Local(B), c0 = Local(C);
 
     // C := 0.5 A B - 0.25 C
@@ -58,7 +76,7 @@ int main() {
     EXPECT(err <= 1e-13 * (ref + 1));
 
     // beta-less form resizes C; transpose orientation: D := A^T A  (k x k)
-    El::DistMatrix<double> D(g);
+    DM<double> D(g);
     El::Gemm(El::TRANSPOSE, El::NORMAL, 1.0, A, A, D, El::GEMM_SUMMA_C);
     EXPECT(D.Height() == k && D.Width() == k);
     auto d = Local(D);
@@ -72,7 +90,7 @@ int main() {
     EXPECT(err <= 1e-12);
 
     // Syrk (beta-less): E := tril(A^T A); its strict upper triangle stays zero
-    El::DistMatrix<double> E(g);
+    DM<double> E(g);
     El::Syrk(El::LOWER, El::TRANSPOSE, 1.0, A, E);
     EXPECT(E.Height() == k && E.Width() == k);
     auto e = Local(E);
@@ -97,7 +115,7 @@ int main() {
         std::vector<double> rhs(k * n);
         for (Int j = 0; j < n; ++j)
             for (Int i = 0; i < k; ++i) rhs[i + j * k] = c_now[(i % m) + j * m];
-        El::DistMatrix<double> Y(k, n, g);
+        DM<double> Y(k, n, g);
         Y.SetLocalBlock(rhs.data(), k);
         El::Trsm(El::LEFT, El::LOWER, El::NORMAL, El::NON_UNIT, 2.0, E, Y);
         const auto y = Local(Y);
@@ -113,12 +131,12 @@ int main() {
     }
 
     // redistribution + transpose + view are bit-exact
-    El::DistMatrix<double, El::STAR, El::STAR> S(A);
+    DM<double, El::STAR, El::STAR> S(A);
     EXPECT(Local(S) == a);
-    El::DistMatrix<double, El::VR, El::STAR> R(g);
+    DM<double, El::VR, El::STAR> R(g);
     R = A;
     EXPECT(Local(R) == a);
-    El::DistMatrix<double> T(g);
+    DM<double> T(g);
     El::Transpose(A, T);
     auto t = Local(T);
     bool tok = T.Height() == k && T.Width() == m;
@@ -127,7 +145,7 @@ int main() {
     EXPECT(tok);
     auto Av = A(El::IR(3, 10), El::IR(5, 9));
     EXPECT(Av.Height() == 7 && Av.Width() == 4 && Av.Viewing());
-    El::DistMatrix<double> W(Av);
+    DM<double> W(Av);
     auto w = Local(W);
     bool vok = true;
     for (Int j = 0; j < 4; ++j)
@@ -135,7 +153,7 @@ int main() {
     EXPECT(vok);
 
     // level-1 front doors
-    El::DistMatrix<double> Y(S);
+    DM<double> Y(S);
     El::Axpy(2.0, A, Y);   // Y = 3A
     El::Scale(0.5, Y);     // Y = 1.5A
     auto y = Local(Y);
@@ -143,7 +161,7 @@ int main() {
     for (size_t i = 0; i < a.size(); ++i) aok &= std::fabs(y[i] - 1.5 * a[i]) <= 1e-15 * std::fabs(a[i]) + 1e-300;
     EXPECT(aok);
     El::EntrywiseMap(A, Y, El::EntrywiseFn::SQUARE);
-    El::DistMatrix<double> H(g);
+    DM<double> H(g);
     H.Resize(m, k);
     El::Hadamard(A, A, H);
     EXPECT(Local(H) == Local(Y));
@@ -158,7 +176,7 @@ int main() {
     for (double v : Local(H)) EXPECT(v == 0.0);
 
     // float path
-    El::DistMatrix<float> Af(8, 8, g), Bf(8, 8, g), Cf(8, 8, g);
+    DM<float> Af(8, 8, g), Bf(8, 8, g), Cf(8, 8, g);
     El::HashFill(Af, 1, 0.0, 1.0);
     El::HashFill(Bf, 2, 0.0, 1.0);
     El::Gemm(El::NORMAL, El::TRANSPOSE, 1.0f, Af, Bf, 0.0f, Cf);
@@ -181,12 +199,15 @@ int main() {
     }
     EXPECT(threw);
 
-    // Attach: caller storage with ldim > height, computed into in place
-    std::vector<double> cbuf((m + 2) * n, 9.0);
-    El::DistMatrix<double> Ca(g);
-    Ca.Attach(m, n, g, 0, 0, cbuf.data(), m + 2);
+    // Attach: caller storage (an El::Matrix on the same device) with ldim > height, computed into in place
+    El::Matrix<double, kDev> Cm(m + 2, n);
+    El::Fill(Cm, 9.0);
+    DM<double> Ca(g);
+    Ca.Attach(m, n, g, 0, 0, Cm.Buffer(), m + 2);
     EXPECT(Ca.Viewing() && Ca.LDim() == m + 2);
     El::Gemm(El::NORMAL, El::NORMAL, 0.5, A, B, 0.0, Ca);
+    Ca.Synchronize();
+    const std::vector<double> cbuf = HostOf(Cm);
     bool tok2 = true;
     for (Int j = 0; j < n; ++j) {
         for (Int i = 0; i < m; ++i) {
@@ -202,10 +223,77 @@ int main() {
     {
         const std::string base = "/tmp/elx_api_test_" + std::to_string(::getpid());
         El::Write(A, base, El::BINARY);
-        El::DistMatrix<double, El::VC, El::STAR> R(g);
+        DM<double, El::VC, El::STAR> R(g);
         El::Read(R, base + ".bin");
         EXPECT(R.Height() == m && R.Width() == k && Local(R) == Local(A));
         std::remove((base + ".bin").c_str());
+    }
+
+    // El::Matrix<T,D> and Gemm on local matrices (level3.hpp:37-65): the local
+    // blocks of A and B through LockedMatrix(), into an owned Matrix
+    {
+        El::Matrix<double, kDev> L(m, n);
+        El::Gemm(El::NORMAL, El::NORMAL, 0.5, A.LockedMatrix(), B.LockedMatrix(), 0.0, L);
+        EXPECT(A.LockedMatrix().Height() == m && A.LockedMatrix().Width() == k && A.LockedMatrix().Viewing());
+        El::Matrix<double, kDev> L2;  // beta-less form resizes
+        El::Gemm(El::TRANSPOSE, El::NORMAL, 1.0, A.LockedMatrix(), A.LockedMatrix(), L2);
+        EXPECT(L2.Height() == k && L2.Width() == k);
+        const auto l = HostOf(L), l2 = HostOf(L2);
+        double lerr = 0;
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) {
+                double s = 0;
+                for (Int q = 0; q < k; ++q) s += a[i + q * m] * b[q + j * k];
+                lerr = std::max(lerr, std::fabs(l[i + j * m] - 0.5 * s));
+            }
+        for (Int j = 0; j < k; ++j)
+            for (Int i = 0; i < k; ++i) lerr = std::max(lerr, std::fabs(l2[i + j * k] - d[i + j * k]));
+        EXPECT(lerr <= 1e-12);
+        // level-1 on Matrix and on the DistMatrix's local block
+        El::Matrix<double, kDev> X(L);  // deep copy
+        El::Axpy(-1.0, L, X);           // X = 0
+        for (double v : HostOf(X)) EXPECT(v == 0.0);
+        El::Scale(2.0, A.Matrix());     // A's local block doubled in place ...
+        EXPECT(A.Get(3, 5) == 2.0 * a[3 + 5 * m]);
+        El::Scale(0.5, A.Matrix());     // ... and back (exact)
+        EXPECT(Local(A) == a);
+        bool threw_k = false;
+        try { El::Gemm(El::NORMAL, El::NORMAL, 1.0, A.LockedMatrix(), A.LockedMatrix(), 0.0, L); }
+        catch (const El::LogicError&) { threw_k = true; }
+        EXPECT(threw_k);
+    }
+
+    // DistMatrix entry access (Get collective, Set / Update local) and El::Fill
+    {
+        EXPECT(A.Get(3, 5) == a[3 + 5 * m] && A.Get(m - 1, k - 1) == a[(m - 1) + (k - 1) * m]);
+        DM<double> F(4, 3, g);
+        El::Fill(F, 2.5);
+        for (double v : Local(F)) EXPECT(v == 2.5);
+        F.Set(1, 2, -7.0);
+        F.Update(1, 2, 0.5);
+        EXPECT(F.Get(1, 2) == -6.5 && F.Get(0, 0) == 2.5);
+        DM<El::gpu_half_type> Hh(3, 3, g);
+        El::Fill(Hh, El::gpu_half_type{0x3c00});  // 1.0
+        Hh.Set(2, 1, El::gpu_half_type{0xc000});   // -2.0
+        EXPECT(Hh.Get(0, 0).x == 0x3c00 && Hh.Get(2, 1).x == 0xc000);
+        DM<El::bfloat16> Bh(2, 2, g);
+        Bh.Set(1, 1, El::bfloat16{0x4040});        // 3.0
+        EXPECT(Bh.Get(1, 1).x == 0x4040);
+    }
+
+    // Trsm's checkIfSingular (Trsm.cpp:60-68): an exact zero on a NON_UNIT
+    // diagonal raises SingularMatrixException; UNIT diagonals are not checked
+    {
+        DM<double> Z(5, 5, g), Y(5, 2, g);
+        El::Fill(Z, 1.0);
+        El::Fill(Y, 1.0);
+        Z.Set(3, 3, 0.0);
+        bool sing = false;
+        try { El::Trsm(El::LEFT, El::LOWER, El::NORMAL, El::NON_UNIT, 1.0, Z, Y, true); }
+        catch (const El::SingularMatrixException&) { sing = true; }
+        EXPECT(sing);
+        El::Trsm(El::LEFT, El::LOWER, El::NORMAL, El::UNIT, 1.0, Z, Y, true);
+        EXPECT(Y.Get(0, 0) == 1.0 && Y.Get(1, 0) == 0.0);
     }
 
     El::SetBlocksize(64);

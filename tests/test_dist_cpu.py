@@ -45,6 +45,46 @@ def test_gemm_f32_grid_2x2():
     _spawn(W.gemm_worker, 4, 2, el.CPU, el.F32, [(17, 21, 15)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 4, 11)
 
 
+@pytest.mark.parametrize("dtype", [el.F64, el.F32])
+def test_gemm_grid_2x4(dtype):
+    """C3's grid shape: 8 ranks as 2x4 (Grid::DefaultHeight(8) = 2), every
+    orientation and algorithm (f32: C and Dot)."""
+    algs = [el.GEMM_DEFAULT, el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT] \
+        if dtype == el.F64 else [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT]
+    _spawn(W.gemm_worker, 8, 2, el.CPU, dtype, [(19, 26, 21)], algs, 4, 13)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2), (8, 2)])
+def test_gemm_multi_panel_pipeline(world, height):
+    """SUMMA_C with the compute panel forced to 8 columns and k = 61: eight panels
+    through the two slots on 1x2 / 2x2 / 2x4 grids, so every slot is regathered
+    while the previous update may still read it (NN.hpp:371-384)."""
+    _spawn(W.gemm_worker, world, height, el.CPU, el.F64, [(21, 18, 61)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_C_MS],
+           4, 19, 8)
+
+
+@pytest.mark.parametrize("dtype", [el.F16, el.BF16])
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_gemm_16bit_distributed(dtype, world, height):
+    """C5's distributed 16-bit El::Gemm on [MC,MR] (f32 accumulation), every
+    orientation and algorithm, against the exact product of the 16-bit inputs."""
+    algs = [el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT]
+    _spawn(W.gemm_worker, world, height, el.CPU, dtype, [(23, 17, 29)], algs, 4, 23)
+
+
+def test_syrk_multi_panel_pipeline():
+    """Syrk/Trrk/Syr2k through the triangular pipeline with 4-column compute
+    panels on a 2x2 grid (k = 30: eight panels)."""
+    _spawn(W.syrk_worker, 4, 2, el.CPU, el.F64, [(23, 30)], 4, 29, 4)
+
+
+def test_host_backend_16bit_sums():
+    """Reduce-scatter / all-reduce of f16 and bf16 on the host backend: the
+    library folds contributions in rank order, each addition in float rounded
+    back to 16 bits (GPUHalfSumFunc, src/core/environment.cpp:135-142)."""
+    _spawn(W.half_sum_worker, 4, 3)
+
+
 @pytest.mark.parametrize("world,height,cols", [(1, 1, 0), (2, 1, 0), (4, 2, 0), (1, 1, 3), (4, 2, 2), (2, 2, 5)])
 def test_syrk_herk(world, height, cols, monkeypatch):
     """El::Syrk / El::Herk LN/LT/UN/UT on 1x1, 1x2, 2x1 and 2x2 grids (Syrk/*.hpp);

@@ -63,6 +63,90 @@ def test_gpu_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.GPU, 17)
 
 
+@pytest.mark.parametrize("dtype,world,height", [(el.F16, 2, 1), (el.BF16, 4, 2), (el.BF16, 1, 1)])
+def test_gpu_summa_16bit(dtype, world, height):
+    """C5: distributed 16-bit El::Gemm on DistMatrix[MC,MR] (MFMA f32 accumulate)
+    through every SUMMA variant, against the exact product (eps 2^-11 / 2^-8)."""
+    algs = [el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT]
+    _spawn(W.gemm_worker, world, height, el.GPU, dtype, [(45, 37, 61)], algs, 16, 31)
+
+
+@pytest.mark.parametrize("dtype", [el.F64, el.F32])
+def test_gpu_summa_grid_2x4(dtype):
+    """C3's 2x4 grid (8 host-staged ranks on the one device)."""
+    algs = [el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT] if dtype == el.F64 \
+        else [el.GEMM_SUMMA_C]
+    _spawn(W.gemm_worker, 8, 2, el.GPU, dtype, [(45, 37, 61)], algs, 8, 37)
+
+
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+def test_gpu_summa_multi_panel_distributed(world, height):
+    """k = 130 with 16-column compute panels: nine panels through the two GPU
+    slots on 1x2 and 2x2 grids; each slot is regathered on the comm stream while
+    the previous MFMA update reads the other (the slot's `done` event fence)."""
+    _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130)], [el.GEMM_SUMMA_C], 16, 43, 16)
+
+
+def test_gpu_syrk_multi_panel_distributed():
+    _spawn(W.syrk_worker, 4, 2, el.GPU, el.F64, [(45, 70)], 16, 47, 16)
+
+
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 1)])
+def test_gpu_cross_device_copies_and_mixed_operands(world, height):
+    """CPU <-> GPU DistMatrix copies both ways across distributions, bit-exact;
+    Gemm / Trsm with operands on different devices (proxied to C's / X's)."""
+    _spawn(W.xdevice_worker, world, height, 53)
+
+
+def test_gpu_operands_on_other_streams():
+    """A and B on caller streams other than C's: the Level-3 drivers fence C's
+    stream after A's/B's queued work on entry and A's/B's after theirs on exit
+    (MultiSync, include/hydrogen/MultiSync.hpp:33-78), so A can be refilled on its
+    own stream right after the call without disturbing the product."""
+    import torch
+    m, n, k = 300, 257, 411
+    g = el.Grid()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    Ah, Bh, Ch = oracle.hash_matrix(m, k, 1), oracle.hash_matrix(k, n, 2), oracle.hash_matrix(m, n, 3)
+    for alg in (el.GEMM_SUMMA_C, el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_DOT):
+        A = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=m, width=k)
+        B = el.DistMatrix(g, el.F64, el.VC, el.STAR, el.GPU, height=k, width=n)
+        C = el.DistMatrix(g, el.F64, el.MC, el.MR, el.GPU, height=m, width=n)
+        A.set_stream(sa.cuda_stream)
+        B.set_stream(sb.cuda_stream)
+        A.fill_hash(1, 0.0, 1.0)   # queued on A's stream
+        B.fill_hash(2, 0.0, 1.0)   # queued on B's stream
+        C.set_local(Ch)
+        el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, alg)
+        A.fill_hash(9, 5.0, 1.0)   # overwrite A on its own stream at once
+        el.device_synchronize()
+        want = oracle.gemm("N", "N", 0.5, Ah, Bh, -0.5, Ch)
+        assert oracle.parity_ratio(C.get_local(), want, Ah, Bh, k, np.finfo(np.float64).eps) <= 10, alg
+
+
+def test_gpu_el_api_cpp(tmp_path):
+    """The drop-in C++ header on Device::GPU matrices (tests/cpp/test_el_api.cpp
+    built with -DEL_TEST_GPU): Gemm, Matrix<T,GPU>/LockedMatrix Gemm, Syrk/Herk,
+    Trsm (+ checkIfSingular), redistributions, Get/Set, Fill, level-1, Attach,
+    Write/Read."""
+    import os
+    import shutil
+    import subprocess
+    from elemental_amd import _lib as L
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "test_el_api_gpu"
+    libdir = os.path.dirname(L.LIB_PATH)
+    subprocess.check_call([gxx, "-std=c++17", "-O1", "-DEL_TEST_GPU", "-I", os.path.join(root, "include"),
+                           os.path.join(root, "tests", "cpp", "test_el_api.cpp"), "-o", str(exe), "-L", libdir,
+                           "-lelemental_amd", f"-Wl,-rpath,{libdir}"])
+    res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "OK" in res.stdout
+
+
 def test_gpu_summa_pipeline_multi_panel():
     """1x1 grid, compute panel < k: several pipelined panels over two slots."""
     m, n, k = 700, 513, 900

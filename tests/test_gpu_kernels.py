@@ -167,6 +167,17 @@ def test_blas1_kernels(t, npdt):
     got = _as_f64(host(dY, (m, n), hostdt), npdt)
     want = _as_f64(_round((Yf + 0.5 * Xf) if t in (L.F64,) else (Yf.astype(np.float32) + np.float32(0.5) * Xf.astype(np.float32)), npdt), npdt)
     assert np.array_equal(got, want)
+    # transposed form (Axpy_GPU_impl with X's strides swapped, Axpy.cu:119-189):
+    # W (n x m) += -1.5 X^T
+    W = _mat(n, m, 33, npdt)
+    Wf = _as_f64(W, npdt)
+    dW = dev(W)
+    torch.cuda.synchronize()
+    L.call("elx_axpy2d", t, n, m, -1.5, dX.data_ptr(), m, 1, dW.data_ptr(), 1, n, None)
+    sync()
+    cdt = np.float64 if t == L.F64 else np.float32
+    wantT = _as_f64(_round(Wf.astype(cdt) + cdt(-1.5) * Xf.T.astype(cdt), npdt), npdt)
+    assert np.array_equal(_as_f64(host(dW, (n, m), hostdt), npdt), wantT)
     # scale, fill, hadamard, entrywise map
     dS = dev(X)
     torch.cuda.synchronize()
@@ -183,6 +194,18 @@ def test_blas1_kernels(t, npdt):
     sync()
     prod = (Xf * Yf) if t == L.F64 else (Xf.astype(np.float32) * Yf.astype(np.float32))
     assert np.array_equal(_as_f64(host(dZ, (m, n), hostdt), npdt), _as_f64(_round(prod, npdt), npdt))
+    # in-place forms (Hadamard.cu:64-116): C aliasing A, and C aliasing both
+    dA2 = dev(X)
+    torch.cuda.synchronize()
+    L.call("elx_hadamard2d", t, m, n, dA2.data_ptr(), m, dY.data_ptr(), m, dA2.data_ptr(), m, None)
+    sync()
+    assert np.array_equal(_as_f64(host(dA2, (m, n), hostdt), npdt), _as_f64(_round(prod, npdt), npdt))
+    dA3 = dev(X)
+    torch.cuda.synchronize()
+    L.call("elx_hadamard2d", t, m, n, dA3.data_ptr(), m, dA3.data_ptr(), m, dA3.data_ptr(), m, None)
+    sync()
+    sq = (Xf * Xf) if t == L.F64 else (Xf.astype(np.float32) * Xf.astype(np.float32))
+    assert np.array_equal(_as_f64(host(dA3, (m, n), hostdt), npdt), _as_f64(_round(sq, npdt), npdt))
     L.call("elx_entrywise_map", t, L.MAP_ABS, m, n, dX.data_ptr(), m, dZ.data_ptr(), m, None)
     sync()
     assert np.array_equal(_as_f64(host(dZ, (m, n), hostdt), npdt), np.abs(Xf))
@@ -218,12 +241,54 @@ def test_fill_hash_bit_exact(t, npdt):
 
 
 def test_pool_alloc_free():
-    p = ctypes.c_void_p()
-    L.call("elx_pool_alloc", ctypes.byref(p), 1 << 20, None)
-    assert p.value
-    L.call("elx_pool_free", p, None)
-    r, u = el.pool_stats()
-    assert u == 0 or u >= 0
+    """The hipMallocAsync pool that replaces hipCUB's CachingDeviceAllocator
+    (src/core/imports/cub.cpp): stream-ordered alloc/free, reuse of freed blocks
+    (the reserved size does not grow on a repeat of the same pattern), blocks
+    freed on one stream and reallocated on another, in-use back to zero, and a
+    trim that returns the cached memory."""
+    el.device_synchronize()
+    _, u0 = el.pool_stats()
+    s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+    L.call("elx_stream_create", ctypes.byref(s1))
+    L.call("elx_stream_create", ctypes.byref(s2))
+    sizes = [1 << 20, 3 << 20, 64 << 20, 5000]
+    try:
+        def round_trip(alloc_stream, free_stream):
+            ptrs = []
+            for b in sizes:
+                p = ctypes.c_void_p()
+                L.call("elx_pool_alloc", ctypes.byref(p), b, alloc_stream)
+                assert p.value and p.value % 256 == 0
+                ptrs.append(p)
+            _, u = el.pool_stats()
+            assert u - u0 == sum(sizes)
+            # the blocks are distinct and writable
+            for p, b in zip(ptrs, sizes):
+                L.call("elx_fill2d", L.F32, b // 4, 1, 1.0, p, max(b // 4, 1), alloc_stream)
+            for p in ptrs:
+                L.call("elx_pool_free", p, free_stream)
+            L.call("elx_stream_synchronize", free_stream)
+            _, u = el.pool_stats()
+            assert u == u0
+
+        round_trip(s1, s1)
+        round_trip(s2, s1)
+        round_trip(s1, s2)
+        r1, _ = el.pool_stats()
+        for _ in range(3):  # freed on s1, reallocated on s2 and back: served from the cache
+            round_trip(s2, s1)
+            round_trip(s1, s2)
+        r2, _ = el.pool_stats()
+        assert r2 == r1, (r1, r2)
+        L.call("elx_pool_trim", 0)
+        r3, _ = el.pool_stats()
+        assert r3 <= r2
+        with pytest.raises(L.LogicError, match="not from this pool"):
+            L.call("elx_pool_free", ctypes.c_void_p(0x1000), None)
+    finally:
+        el.device_synchronize()
+        L.call("elx_stream_destroy", s1)
+        L.call("elx_stream_destroy", s2)
 
 
 @pytest.mark.parametrize("s", [L.F64, L.F32, L.F16, L.BF16])
