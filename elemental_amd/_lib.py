@@ -135,6 +135,8 @@ _SIGS = {
     "elx_blocksize": (_i64, []),
     "elx_set_compute_panel": (_i, [_i64]),
     "elx_last_gemm_algorithm": (_i, []),
+    "elx_set_stream_pool_size": (_i, [_i]),
+    "elx_stream_pool_size": (_i, []),
     "elx_set_profiling": (_i, [_i]),
     "elx_profile_stats": (_i, [POINTER(c_double), POINTER(c_int64), POINTER(c_double), POINTER(c_double),
                                POINTER(c_int64)]),

@@ -436,6 +436,8 @@ int elx_set_blocksize(int64_t nb) { return Guard([&] { SetBlocksize(nb); }); }
 int64_t elx_blocksize(void) { return Blocksize(); }
 int elx_set_compute_panel(int64_t kc) { return Guard([&] { SetComputePanel(kc); }); }
 int elx_last_gemm_algorithm(void) { return LastGemmAlgorithm(); }
+int elx_set_stream_pool_size(int n) { return Guard([&] { SetStreamPoolSize(n); }); }
+int elx_stream_pool_size(void) { return StreamPoolSize(); }
 int elx_set_profiling(int on) { return Guard([&] { SetProfiling(on != 0); }); }
 int elx_profile_stats(double* gemm_ms, int64_t* launches, double* flops, double* comm_ms, int64_t* bytes) {
     return Guard([&] { ProfileStats(*gemm_ms, *launches, *flops, *comm_ms, *bytes); });

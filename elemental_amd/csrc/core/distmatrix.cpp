@@ -300,6 +300,15 @@ std::shared_ptr<DistMatrix> DistMatrix::View(const DistMatrix& A, Int i0, Int i1
     return V;
 }
 
+std::shared_ptr<DistMatrix> DistMatrix::ViewOn(const DistMatrix& A, std::shared_ptr<Grid> g) {
+    ELX_REQUIRE(g && g->Height() == A.G().Height() && g->Width() == A.G().Width() &&
+                    g->VCRank() == A.G().VCRank() && g->Order() == A.G().Order(),
+                "ViewOn: grids differ in shape or rank");
+    auto V = View(A, 0, A.h_, 0, A.w_);
+    V->grid_ = std::move(g);
+    return V;
+}
+
 void DistMatrix::SetSyncStream(hipStream_t s) {
     if (dev_ != Device::GPU || s == stream_) return;
     hipEvent_t ev;

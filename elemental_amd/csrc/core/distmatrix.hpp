@@ -60,6 +60,7 @@ public:
     Comm& VC() const { return *vc_comm_; }
     Comm& VR() const { return *vr_comm_; }
     Comm& World() const { return *world_; }
+    std::shared_ptr<Comm> WorldPtr() const { return world_; }
     Device CommDevice() const;  // where the comms expect buffers (GPU for RCCL)
     int Order() const { return order_; }
 
@@ -135,6 +136,9 @@ public:
     void Attach(Int height, Int width, int colAlign, int rowAlign, void* buffer, Int ldim, int root);
     // V := A(i0:i1, j0:j1), sharing A's storage
     static std::shared_ptr<DistMatrix> View(const DistMatrix& A, Int i0, Int i1, Int j0, Int j1);
+    // all of A, sharing A's storage, on another Grid object of the same shape and
+    // rank (a multistream team's grid, whose communicators are duplicates)
+    static std::shared_ptr<DistMatrix> ViewOn(const DistMatrix& A, std::shared_ptr<Grid> g);
     // fresh matrix with the same grid/type/device
     std::shared_ptr<DistMatrix> Like(Dist cd, Dist rd) const;
     // same grid/type on device `dev` (this matrix's stream when the device matches)

@@ -19,8 +19,11 @@
 //    local views), so the fp64 update runs at k >= 2048 instead of k = 128 and
 //    C's HBM round trip per panel stays a few % of the MFMA time.  Only the
 //    summation order changes (normwise tolerance); data movement is bit-exact.
-//  * the _MS algorithm ids run the same pipelined variants (the reference's
-//    ROCm build rejects NT/TN _MS, TN.hpp:124-128).
+//  * the _MS algorithm ids are the reference's multistream variants: with a
+//    stream pool (H_STREAMPOOL_SIZE > 1) panels round-robin over teams, each with
+//    its own stream and duplicated RCCL communicators (SummaCMultistream,
+//    SummaA/SummaB with teams); NT/TN included (the reference's ROCm build
+//    rejects those, TN.hpp:124-128).
 #include "gemm.hpp"
 #include <cstdlib>
 #include "redist.hpp"
@@ -154,6 +157,123 @@ struct RWProxy {
 
 void Check(bool cond, const char* what) {
     if (!cond) throw LogicError(Cat("LocalGemm: ", what));
+}
+
+// ---------------------------------------------------------------------------
+// Multistream teams: hydrogen::SyncInfoPool (SyncInfoPool.hpp:23-195) and
+// GetSyncInfoPool / InitializeComms (Gemm.cpp:17-90).  H_STREAMPOOL_SIZE
+// streams, each with its own duplicate of the grid's communicators: an RCCL
+// communicator's operations are ordered, so concurrent panels on different
+// streams need different communicators (the reference gets one Aluminum
+// communicator per SyncInfo the same way).  Built collectively, once per grid,
+// on first use.  A host-backend grid (blocking collectives, program order) is
+// shared by every team; only the streams differ.
+// ---------------------------------------------------------------------------
+int g_pool_size = -1;  // -1: read H_STREAMPOOL_SIZE (Gemm.cpp:22-29, default 1)
+
+struct Team {
+    std::shared_ptr<Grid> grid;
+    hipStream_t stream = nullptr;
+};
+struct TeamSet {
+    std::weak_ptr<Grid> base;
+    std::vector<Team> teams;
+};
+
+std::vector<TeamSet>& TeamCache() {
+    static auto* c = new std::vector<TeamSet>();  // leaked: outlives static destructors
+    return *c;
+}
+
+const std::vector<Team>& Teams(const std::shared_ptr<Grid>& g, Device dev, int n) {
+    auto& cache = TeamCache();
+    for (auto it = cache.begin(); it != cache.end();) {  // drop teams of destroyed grids
+        if (it->base.expired()) {
+            for (auto& t : it->teams)
+                if (t.stream) (void)hipStreamDestroy(t.stream);
+            it = cache.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    TeamSet* ts = nullptr;
+    for (auto& e : cache)
+        if (e.base.lock() == g) ts = &e;
+    if (!ts) {
+        cache.push_back(TeamSet{g, {}});
+        ts = &cache.back();
+    }
+    const bool gpu = dev == Device::GPU;
+    while (static_cast<int>(ts->teams.size()) < n) {
+        Team t;
+        if (g->World().kind() == Comm::Kind::RCCL) {
+            auto dup = g->WorldPtr()->Split(0, g->World().Rank());  // collective on every rank
+            t.grid = std::make_shared<Grid>(dup, g->Height(), g->Order());
+        } else {
+            t.grid = g;
+        }
+        if (gpu) ELX_CHECK_HIP(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
+        ts->teams.push_back(t);
+    }
+    if (gpu)
+        for (auto& t : ts->teams)
+            if (!t.stream) ELX_CHECK_HIP(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
+    return ts->teams;
+}
+
+// Per-team views of the (proxied) operands: team t's A, B and C are views on
+// its grid, queued on its stream, every team stream ordered after C's stream on
+// entry.  S == 1: the operands themselves.
+struct TeamViews {
+    struct V {
+        std::shared_ptr<const DistMatrix> A, B;
+        std::shared_ptr<DistMatrix> C;
+        hipStream_t s = nullptr;
+    };
+    std::vector<V> v;
+    hipStream_t cs;
+    TeamViews(const DistMatrix& A, const DistMatrix& B, DistMatrix& C, int S) : cs(C.Stream()) {
+        if (S <= 1) {
+            v.push_back({std::shared_ptr<const DistMatrix>(&A, [](const DistMatrix*) {}),
+                         std::shared_ptr<const DistMatrix>(&B, [](const DistMatrix*) {}),
+                         std::shared_ptr<DistMatrix>(&C, [](DistMatrix*) {}), cs});
+            return;
+        }
+        const auto& teams = Teams(C.GridPtr(), C.Dev(), S);
+        for (int t = 0; t < S; ++t) {
+            V x;
+            x.s = teams[t].stream;
+            FenceStreams(cs, x.s);
+            auto a = DistMatrix::ViewOn(A, teams[t].grid);
+            auto b = DistMatrix::ViewOn(B, teams[t].grid);
+            x.C = DistMatrix::ViewOn(C, teams[t].grid);
+            a->SetStream(x.s);
+            b->SetStream(x.s);
+            x.C->SetStream(x.s);
+            x.A = a;
+            x.B = b;
+            v.push_back(x);
+        }
+    }
+    const V& operator[](Int p) const { return v[static_cast<size_t>(p % static_cast<Int>(v.size()))]; }
+    // C's stream waits for every team
+    void Join() const {
+        for (auto& x : v) FenceStreams(x.s, cs);
+    }
+    // teams' temporaries are released on their streams: order them after C's
+    ~TeamViews() {
+        for (auto& x : v) {
+            try { FenceStreams(cs, x.s); } catch (...) {}
+        }
+    }
+};
+
+// number of teams for `panels` panels (NN_Multistream.hpp:288-291: the pool
+// size, at most one team per panel; a pool of one means no teams)
+int TeamCount(const DistMatrix& C, Int panels) {
+    const int pool = StreamPoolSize();
+    if (C.Dev() != Device::GPU || pool <= 1) return 1;
+    return static_cast<int>(std::max<Int>(1, std::min<Int>(pool, panels)));
 }
 
 Int EffectivePanel(const Grid& g, Int K, DType t) {
@@ -398,19 +518,109 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 }
 
 // ---------------------------------------------------------------------------
-// A-stationary (keeps A, reduces partial C panels): NN.hpp:107-154, NT.hpp:19-59,
-// TN.hpp:19-61, TT.hpp:17-61.  Loop over column panels of C.
+// C-stationary multistream (NN_Multistream.hpp:262-412, NT/TN siblings): panel
+// p is gathered and applied by team p mod S, each on its own stream with its own
+// communicators, panel slots and copy of C (team 0 updates C itself, the others
+// zero-initialised copies, NN_Multistream.hpp:340-355), summed into C at the end
+// (:408-411).  Panels are ComputePanel() deep, as in the pipelined driver.
 // ---------------------------------------------------------------------------
-void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+void SummaCMultistream(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
+                       DistMatrix& CPre) {
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
-    const DistMatrix& A = *Ap;
-    const DistMatrix& B = *Bp;
-    DistMatrix& C = Cp.Get();
-    const Int n = C.Width(), nb = g_blocksize;
+    DistMatrix& C0 = Cp.Get();
+    const Int K = IsN(oA) ? Ap->Width() : Ap->Height();
+    const Int kc = EffectivePanel(C0.G(), K, C0.Type());
+    const Int np = (K + kc - 1) / kc;
+    Scale(beta, C0);  // Gemm.cpp:282; the team copies start from zero
+    TeamViews tv(*Ap, *Bp, C0, TeamCount(C0, np));
+    const int S = static_cast<int>(tv.v.size());
+    const Dist a_cd = IsN(oA) ? Dist::MC : Dist::STAR, a_rd = IsN(oA) ? Dist::STAR : Dist::MC;
+    const Dist b_cd = IsN(oB) ? Dist::STAR : Dist::MR, b_rd = IsN(oB) ? Dist::MR : Dist::STAR;
+    struct TeamData { std::shared_ptr<DistMatrix> c, a, b; };
+    std::vector<TeamData> td(S);
+    for (int t = 0; t < S; ++t) {
+        const DistMatrix& Ct = *tv.v[t].C;
+        if (t == 0) {
+            td[t].c = tv.v[t].C;
+        } else {
+            td[t].c = Ct.Like(Dist::MC, Dist::MR);
+            td[t].c->Align(Ct.ColAlign(), Ct.RowAlign(), true);
+            td[t].c->Resize(Ct.Height(), Ct.Width());
+            Zero(*td[t].c);
+        }
+        td[t].a = tv.v[t].A->Like(a_cd, a_rd);
+        td[t].b = tv.v[t].B->Like(b_cd, b_rd);
+        if (IsN(oA)) td[t].a->AlignCols(Ct.ColAlign(), true); else td[t].a->AlignRows(Ct.ColAlign(), true);
+        if (IsN(oB)) td[t].b->AlignRows(Ct.RowAlign(), true); else td[t].b->AlignCols(Ct.RowAlign(), true);
+    }
+    const Device dev = C0.Dev();
+    const int call_id = Prof().calls++;
+    for (Int p = 0; p < np; ++p) {
+        const int t = static_cast<int>(p % S);
+        const auto& v = tv.v[t];
+        const DistMatrix& A = *v.A;
+        const DistMatrix& B = *v.B;
+        DistMatrix& Ct = *td[t].c;
+        const Int k0 = p * kc, k1 = std::min(K, k0 + kc);
+        auto Av = IsN(oA) ? DistMatrix::View(A, 0, A.Height(), k0, k1) : DistMatrix::View(A, k0, k1, 0, A.Width());
+        auto Bv = IsN(oB) ? DistMatrix::View(B, k0, k1, 0, B.Width()) : DistMatrix::View(B, 0, B.Height(), k0, k1);
+        std::shared_ptr<const DistMatrix> ua = Av, ub = Bv;
+        if (!SameLocalLayout(*Av, a_cd, a_rd, td[t].a->ColAlign(), td[t].a->RowAlign())) {
+            Copy(*Av, *td[t].a);
+            ua = td[t].a;
+        }
+        if (!SameLocalLayout(*Bv, b_cd, b_rd, td[t].b->ColAlign(), td[t].b->RowAlign())) {
+            Copy(*Bv, *td[t].b);
+            ub = td[t].b;
+        }
+        const Int m = Ct.LocalHeight(), n = Ct.LocalWidth();
+        const Int k = IsN(oA) ? ua->LocalWidth() : ua->LocalHeight();
+        if (m > 0 && n > 0 && k > 0) {
+            const bool prof = dev == Device::GPU && Prof().on;
+            Profiler::Rec rec{};
+            if (prof) rec = Prof().Begin(v.s);
+            exec::Gemm(dev, Ct.Type(), !IsN(oA), !IsN(oB), m, n, k, alpha, ua->Buffer(), ua->LDim(), ub->Buffer(),
+                       ub->LDim(), 1.0, Ct.Buffer(), Ct.LDim(), v.s);
+            if (prof) Prof().End(rec, v.s, 2.0 * m * n * k, Prof().gemm, call_id);
+        }
+    }
+    tv.Join();
+    // C += sum of the other teams' copies (in team order, on C's stream)
+    for (int t = 1; t < S; ++t) {
+        const DistMatrix& Ct = *td[t].c;
+        if (C0.LocalHeight() == 0 || C0.LocalWidth() == 0) break;
+        kern::Copy2D d{C0.LocalHeight(), C0.LocalWidth(), Ct.Buffer(), 1, Ct.LDim(), C0.Buffer(), 1, C0.LDim()};
+        exec::Copy2DBatch(dev, C0.Type(), &d, 1, true, 1.0, C0.Stream());
+    }
+    // the copies are released on their teams' streams: after the sums read them
+    for (auto& x : tv.v) FenceStreams(tv.cs, x.s);
+    td.clear();
+    Cp.Finish();
+}
+
+// ---------------------------------------------------------------------------
+// A-stationary (keeps A, reduces partial C panels): NN.hpp:107-154, NT.hpp:19-59,
+// TN.hpp:19-61, TT.hpp:17-61.  Loop over column panels of C.
+// ---------------------------------------------------------------------------
+// ms: the multistream variant (NN_Multistream.hpp:5-130 and the NT/TN
+// siblings): panel p runs on team p mod S, each team with its own stream,
+// communicators and temporaries; the C panels are disjoint, so no C copies.
+void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
+            bool ms = false) {
+    MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
+    auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
+    auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
+    RWProxy Cp(CPre);
+    const Int n = Cp.Get().Width(), nb = std::max<Int>(1, g_blocksize);
+    TeamViews tv(*Ap, *Bp, Cp.Get(), ms ? TeamCount(Cp.Get(), (n + nb - 1) / nb) : 1);
     for (Int k = 0; k < n; k += nb) {
+        const auto& tm = tv[k / nb];
+        const DistMatrix& A = *tm.A;
+        const DistMatrix& B = *tm.B;
+        DistMatrix& C = *tm.C;
         const Int k1 = std::min(n, k + nb);
         auto C1 = DistMatrix::View(C, 0, C.Height(), k, k1);
         if (IsN(oA)) {
@@ -435,6 +645,7 @@ void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             AxpyContract(1.0, *D1, *C1);  // [MR,*] -> [MC,MR]: reduce over MC + exchange
         }
     }
+    tv.Join();
     Cp.Finish();
 }
 
@@ -442,16 +653,19 @@ void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // B-stationary (keeps B, reduces partial C row panels): NN.hpp:226-270,
 // NT.hpp:134-176, TN.hpp:137-176, TT.hpp:105-152.  Loop over row panels of C.
 // ---------------------------------------------------------------------------
-void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
+            bool ms = false) {
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
-    const DistMatrix& A = *Ap;
-    const DistMatrix& B = *Bp;
-    DistMatrix& C = Cp.Get();
-    const Int m = C.Height(), nb = g_blocksize;
+    const Int m = Cp.Get().Height(), nb = std::max<Int>(1, g_blocksize);
+    TeamViews tv(*Ap, *Bp, Cp.Get(), ms ? TeamCount(Cp.Get(), (m + nb - 1) / nb) : 1);
     for (Int k = 0; k < m; k += nb) {
+        const auto& tm = tv[k / nb];
+        const DistMatrix& A = *tm.A;
+        const DistMatrix& B = *tm.B;
+        DistMatrix& C = *tm.C;
         const Int k1 = std::min(m, k + nb);
         auto C1 = DistMatrix::View(C, k, k1, 0, C.Width());
         // op(A)1 = rows k..k1 of op(A)
@@ -476,6 +690,7 @@ void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             AxpyContract(1.0, *D1, *C1);
         }
     }
+    tv.Join();
     Cp.Finish();
 }
 
@@ -588,6 +803,15 @@ Int Blocksize() { return g_blocksize; }
 void SetComputePanel(Int kc) { ELX_REQUIRE(kc >= 0, "compute panel must be >= 0"); g_compute_panel = kc; }
 Int ComputePanel() { return g_compute_panel; }
 int LastGemmAlgorithm() { return g_last_alg; }
+void SetStreamPoolSize(int n) {
+    ELX_REQUIRE(n >= 0, "stream pool size must be >= 0 (0: H_STREAMPOOL_SIZE)");
+    g_pool_size = n == 0 ? -1 : n;
+}
+int StreamPoolSize() {
+    if (g_pool_size > 0) return g_pool_size;
+    const char* e = getenv("H_STREAMPOOL_SIZE");
+    return e && atoi(e) > 0 ? atoi(e) : 1;
+}
 
 void SetProfiling(bool on) {
     if (Runtime::Get().GPUInitialized()) ELX_CHECK_HIP(hipDeviceSynchronize());
@@ -911,13 +1135,31 @@ void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B
     const Int kb = IsN(oB) ? B.Height() : B.Width(), n = IsN(oB) ? B.Width() : B.Height();
     ELX_REQUIRE(m == C.Height() && n == C.Width() && k == kb, "Gemm: nonconformal ", m, "x", k, " * ", kb, "x", n,
                 " -> ", C.Height(), "x", C.Width());
-    if (alg == ELX_GEMM_DEFAULT) alg = Heuristic(m, n, k);
-    const bool fused_beta = alg == ELX_GEMM_SUMMA_C || alg == ELX_GEMM_SUMMA_C_MS;
-    if (!fused_beta) Scale(beta, C);  // Gemm.cpp:282
+    const bool tt = !IsN(oA) && !IsN(oB);
+    // NN.hpp:583-600: with a GPU C and a stream pool larger than one, the
+    // heuristic picks the multistream variants (TT has none, TT.hpp:410-433)
+    const bool gpu_pool = C.Dev() == Device::GPU && TeamCount(C, 2) > 1 && !tt;
+    if (alg == ELX_GEMM_DEFAULT) {
+        alg = Heuristic(m, n, k);
+        if (gpu_pool && alg == ELX_GEMM_SUMMA_A) alg = ELX_GEMM_SUMMA_A_MS;
+        if (gpu_pool && alg == ELX_GEMM_SUMMA_B) alg = ELX_GEMM_SUMMA_B_MS;
+        if (gpu_pool && alg == ELX_GEMM_SUMMA_C) alg = ELX_GEMM_SUMMA_C_MS;
+    }
+    const bool ms = alg == ELX_GEMM_SUMMA_A_MS || alg == ELX_GEMM_SUMMA_B_MS || alg == ELX_GEMM_SUMMA_C_MS;
+    if (ms && tt) throw LogicError("Unsupported Gemm option");  // TT.hpp:433
+    // a CPU C runs the plain variant (the reference warns "CPU doesn't support
+    // multistream variants", TN.hpp:114-118); so does a pool of one
+    const bool teams = ms && C.Dev() == Device::GPU && TeamCount(C, 2) > 1;
+    const bool fused_beta = alg == ELX_GEMM_SUMMA_C || (alg == ELX_GEMM_SUMMA_C_MS && !teams);
+    if (!fused_beta && !(alg == ELX_GEMM_SUMMA_C_MS && teams)) Scale(beta, C);  // Gemm.cpp:282
     switch (alg) {
-    case ELX_GEMM_SUMMA_A_MS: case ELX_GEMM_SUMMA_A: SummaA(oA, oB, alpha, A, B, C); break;
-    case ELX_GEMM_SUMMA_B_MS: case ELX_GEMM_SUMMA_B: SummaB(oA, oB, alpha, A, B, C); break;
-    case ELX_GEMM_SUMMA_C_MS: case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, beta, C); break;
+    case ELX_GEMM_SUMMA_A_MS: case ELX_GEMM_SUMMA_A: SummaA(oA, oB, alpha, A, B, C, teams); break;
+    case ELX_GEMM_SUMMA_B_MS: case ELX_GEMM_SUMMA_B: SummaB(oA, oB, alpha, A, B, C, teams); break;
+    case ELX_GEMM_SUMMA_C_MS:
+        if (teams) SummaCMultistream(oA, oB, alpha, A, B, beta, C);
+        else SummaC(oA, oB, alpha, A, B, beta, C);
+        break;
+    case ELX_GEMM_SUMMA_C: SummaC(oA, oB, alpha, A, B, beta, C); break;
     case ELX_GEMM_SUMMA_DOT:
         SummaDot(oA, oB, alpha, A, B, C, C.Dev() == Device::GPU ? DotBlockGPU() : kDotBlock);
         break;

@@ -36,6 +36,9 @@ Int Blocksize();
 void SetComputePanel(Int kc);
 Int ComputePanel();
 int LastGemmAlgorithm();
+// stream pool of the multistream variants (hydrogen::SyncInfoPool); 0 = H_STREAMPOOL_SIZE
+void SetStreamPoolSize(int n);
+int StreamPoolSize();
 void SetProfiling(bool on);
 void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& comm_ms, int64_t& bytes);
 void CommProfileStats(double& transfer_ms, int64_t& bytes, int64_t& transfers);

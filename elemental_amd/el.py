@@ -405,6 +405,15 @@ def SetComputePanel(kc: int):
     call("elx_set_compute_panel", kc)
 
 
+def SetStreamPoolSize(n: int):
+    """Size of the multistream pool (H_STREAMPOOL_SIZE; 0 = read the variable)."""
+    call("elx_set_stream_pool_size", n)
+
+
+def StreamPoolSize() -> int:
+    return lib().elx_stream_pool_size()
+
+
 def comm_stats() -> dict:
     b, s, c = c_int64(), c_double(), c_int64()
     call("elx_comm_stats", byref(b), byref(s), byref(c))

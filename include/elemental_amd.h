@@ -363,6 +363,12 @@ int64_t elx_blocksize(void);
 int elx_set_compute_panel(int64_t kpanel);
 /* algorithm the last elx_gemm call actually ran (after the heuristic) */
 int elx_last_gemm_algorithm(void);
+/* stream pool of the multistream (_MS) variants: hydrogen::SyncInfoPool and
+ * H_STREAMPOOL_SIZE (src/blas_like/level3/SyncInfoPool.hpp:23-195, Gemm.cpp:17-90).
+ * n > 1: GEMM_DEFAULT on GPU matrices picks SUMMA_{A,B,C}_MS and panels run on
+ * n streams with duplicated RCCL communicators; 0 = read H_STREAMPOOL_SIZE */
+int elx_set_stream_pool_size(int n);
+int elx_stream_pool_size(void);
 /* Profiling (replaces AUTO_PROFILE_REGION/NVTX ranges, include/El/core/Profiling.hpp:143-264):
  * when on, every local MFMA update and every panel transfer issued by the SUMMA
  * drivers is bracketed by HIP events on the stream it runs on.  stats: summed

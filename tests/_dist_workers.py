@@ -100,13 +100,19 @@ def _host_dt(dtype):
     return {0: np.float32, 1: np.float64, 2: np.float16, 3: "bf16"}[dtype]
 
 
+MS_ALGS = (1, 3, 5)  # GEMM_SUMMA_A_MS, GEMM_SUMMA_B_MS, GEMM_SUMMA_C_MS (level3.hpp:22-35)
+
+
 def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtype: int, shapes, algs,
-                nb: int, seed: int, kc: int = 0):
+                nb: int, seed: int, kc: int = 0, pool: int = 0):
     """El::Gemm NN/NT/TN/TT x `algs` against the oracle (north_star normwise
     tolerance).  kc > 0 forces the C-stationary compute panel to kc columns, so
     k >= 2 kc runs several panels through the two-slot pipeline: on grids larger
     than 1x1 every slot is refilled (gathered) while the previous update may still
-    read it (the write-after-read fence of NN.hpp:371-384's loop)."""
+    read it (the write-after-read fence of NN.hpp:371-384's loop).  pool > 1
+    sets the multistream pool (H_STREAMPOOL_SIZE): the _MS ids then run on that
+    many streams (GPU), and GEMM_DEFAULT picks them (NN.hpp:583-600); TT rejects
+    the _MS ids (TT.hpp:410-433)."""
     import oracle
     el, comm = init(rank, world, port)
     try:
@@ -116,6 +122,7 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
         npdt = _host_dt(dtype)
         el.SetBlocksize(nb)
         el.SetComputePanel(kc)
+        el.SetStreamPoolSize(pool)
         for (m, n, k) in shapes:
             for oA in (el.NORMAL, el.TRANSPOSE):
                 for oB in (el.NORMAL, el.TRANSPOSE):
@@ -135,7 +142,16 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
                         A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
                         B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
                         C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+                        if alg in MS_ALGS and oA != el.NORMAL and oB != el.NORMAL:
+                            try:
+                                el.Gemm(oA, oB, alpha, A, B, beta, C, alg)
+                                raise AssertionError("TT with a multistream id must raise")
+                            except el.L.LogicError:
+                                continue
                         ran = el.Gemm(oA, oB, alpha, A, B, beta, C, alg)
+                        if pool > 1 and device == el.GPU and alg == el.GEMM_DEFAULT and \
+                                not (oA != el.NORMAL and oB != el.NORMAL):
+                            assert ran in MS_ALGS + (el.GEMM_SUMMA_DOT,), ran
                         got = oracle.to_f64(C.get_local(), fmt)
                         want = oracle.local_block(ref, el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
                         # north_star normwise bound, applied blockwise with the global norms
@@ -145,6 +161,7 @@ def gemm_worker(rank: int, world: int, port: int, height: int, device: int, dtyp
                             f"Gemm {fmt} {ORIENTS[oA]}{ORIENTS[oB]} alg {alg}->{ran} {m}x{n}x{k} kc {kc} "
                             f"grid {r}x{c} rank {rank}: {num / den:.3g}")
         el.SetComputePanel(0)
+        el.SetStreamPoolSize(0)
         finish()
     except Exception:
         traceback.print_exc()

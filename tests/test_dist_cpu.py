@@ -22,6 +22,13 @@ def _spawn(fn, world, *args):
     mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
 
 
+def test_gemm_multistream_ids_on_cpu():
+    """_MS ids on Device::CPU matrices run the plain variants (the reference warns
+    "CPU doesn't support multistream variants", TN.hpp:114-118); TT rejects them."""
+    algs = [el.GEMM_SUMMA_A_MS, el.GEMM_SUMMA_B_MS, el.GEMM_SUMMA_C_MS, el.GEMM_DEFAULT]
+    _spawn(W.gemm_worker, 2, 1, el.CPU, el.F64, [(19, 13, 23)], algs, 4, 61, 8, 3)
+
+
 @pytest.mark.parametrize("world,height", [(2, 1), (2, 2), (4, 2), (8, 2)])
 def test_redistribution_all_pairs_bit_exact(world, height):
     """tests/core/DistMatrix.cpp: every [X,Y] <- [U,V] of the 14 distributions

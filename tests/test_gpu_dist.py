@@ -87,6 +87,17 @@ def test_gpu_summa_multi_panel_distributed(world, height):
     _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130)], [el.GEMM_SUMMA_C], 16, 43, 16)
 
 
+@pytest.mark.parametrize("world,height,pool", [(1, 1, 2), (2, 1, 3), (4, 2, 2)])
+def test_gpu_summa_multistream(world, height, pool):
+    """GEMM_SUMMA_{A,B,C}_MS with a stream pool (H_STREAMPOOL_SIZE = pool):
+    panels round-robin over teams with their own streams (and per-team C copies
+    for C_MS, summed at the end, NN_Multistream.hpp:340-411) for NN, NT and TN;
+    GEMM_DEFAULT picks the _MS variants; TT rejects them (TT.hpp:410-433).
+    k = 130 with 16-column panels: nine C_MS panels over the teams."""
+    algs = [el.GEMM_DEFAULT, el.GEMM_SUMMA_A_MS, el.GEMM_SUMMA_B_MS, el.GEMM_SUMMA_C_MS]
+    _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130), (16, 12, 70)], algs, 16, 59, 16, pool)
+
+
 def test_gpu_syrk_multi_panel_distributed():
     _spawn(W.syrk_worker, 4, 2, el.GPU, el.F64, [(45, 70)], 16, 47, 16)
 
@@ -201,6 +212,9 @@ def test_gpu_rccl_single_rank_redistribution_and_summa():
     splits, the self-copy paths) - the only RCCL shape a 1-GPU box can run."""
     _rccl_spawn(W.redist_worker, 1, 1, el.GPU, el.F64, 13, 11, 77)
     _rccl_spawn(W.gemm_worker, 1, 1, el.GPU, el.F64, [(45, 37, 61)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 16, 5)
+    # multistream teams over RCCL: each team's grid is a split duplicate of the world
+    _rccl_spawn(W.gemm_worker, 1, 1, el.GPU, el.F64, [(45, 37, 61)],
+                [el.GEMM_SUMMA_C_MS, el.GEMM_SUMMA_A_MS, el.GEMM_DEFAULT], 16, 7, 16, 3)
 
 
 @pytest.mark.skipif(el.device_count() < 2, reason="needs >= 2 GPUs (one RCCL rank per GPU)")
@@ -210,6 +224,8 @@ def test_gpu_rccl_multi_gpu(world, height):
     _rccl_spawn(W.redist_worker, world, min(height, world), el.GPU, el.F64, 13, 11, 99)
     algs = [el.GEMM_SUMMA_A, el.GEMM_SUMMA_B, el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT]
     _rccl_spawn(W.gemm_worker, world, min(height, world), el.GPU, el.F64, [(45, 37, 61)], algs, 16, 6)
+    _rccl_spawn(W.gemm_worker, world, min(height, world), el.GPU, el.F64, [(45, 37, 130)],
+                [el.GEMM_SUMMA_C, el.GEMM_SUMMA_C_MS, el.GEMM_SUMMA_A_MS], 16, 8, 16, 2)
 
 
 def test_gpu_attach_torch_storage():

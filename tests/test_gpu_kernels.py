@@ -168,15 +168,16 @@ def test_blas1_kernels(t, npdt):
     want = _as_f64(_round((Yf + 0.5 * Xf) if t in (L.F64,) else (Yf.astype(np.float32) + np.float32(0.5) * Xf.astype(np.float32)), npdt), npdt)
     assert np.array_equal(got, want)
     # transposed form (Axpy_GPU_impl with X's strides swapped, Axpy.cu:119-189):
-    # W (n x m) += -1.5 X^T
+    # W (n x m) += -2 X^T (a power-of-two alpha: the product is exact, so a fused
+    # multiply-add and the numpy restatement round identically)
     W = _mat(n, m, 33, npdt)
     Wf = _as_f64(W, npdt)
     dW = dev(W)
     torch.cuda.synchronize()
-    L.call("elx_axpy2d", t, n, m, -1.5, dX.data_ptr(), m, 1, dW.data_ptr(), 1, n, None)
+    L.call("elx_axpy2d", t, n, m, -2.0, dX.data_ptr(), m, 1, dW.data_ptr(), 1, n, None)
     sync()
     cdt = np.float64 if t == L.F64 else np.float32
-    wantT = _as_f64(_round(Wf.astype(cdt) + cdt(-1.5) * Xf.T.astype(cdt), npdt), npdt)
+    wantT = _as_f64(_round(Wf.astype(cdt) + cdt(-2.0) * Xf.T.astype(cdt), npdt), npdt)
     assert np.array_equal(_as_f64(host(dW, (n, m), hostdt), npdt), wantT)
     # scale, fill, hadamard, entrywise map
     dS = dev(X)
