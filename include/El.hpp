@@ -358,7 +358,9 @@ public:
     void Align(int colAlign, int rowAlign, bool constrain = true) {
         detail::Check(elx_dm_align(h(), colAlign, rowAlign, constrain));
     }
-    void AlignWith(const AbstractDistMatrix<T>& other, bool constrain = true) {
+    // (any element type: alignment is distribution data, DistData in the reference)
+    template <typename S>
+    void AlignWith(const AbstractDistMatrix<S>& other, bool constrain = true) {
         detail::Check(elx_dm_align_with(h(), other.h(), constrain));
     }
     // ElementalMatrix::Attach: view caller storage as this rank's local block
@@ -659,3 +661,9 @@ inline void Initialize(int&, char**&) { InitializeRandom(true, 0); }
 inline void Finalize() {}
 
 }  // namespace El
+
+// functor-generic EntrywiseMap / Combine on GPU matrices: device templates,
+// available when the caller compiles with hipcc (EntrywiseMap.hpp:141-203)
+#if defined(__HIPCC__)
+#include "El/EntrywiseMap.hip.hpp"
+#endif

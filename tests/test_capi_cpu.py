@@ -152,3 +152,14 @@ def test_uniform_reproduces_reference_draws(dt, kind):
     got = B.get_local()
     assert np.array_equal(got.view(np.uint16) if kind in ("f16", "bf16") else got,
                           nxt.view(np.uint16) if kind == "f16" else nxt)
+
+
+def test_functor_header_compiles_for_gfx950(tmp_path):
+    """include/El/EntrywiseMap.hip.hpp through El.hpp under hipcc (the caller's
+    compiler): a device lambda map/combine instantiates and codegens for gfx950."""
+    hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    subprocess.check_call([hipcc, "-std=c++17", "-O1", "--offload-arch=gfx950", "-c", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "test_entrywise_functor.hip"), "-o",
+                           str(tmp_path / "t.o")])

@@ -135,27 +135,30 @@ def test_gpu_operands_on_other_streams():
         assert oracle.parity_ratio(C.get_local(), want, Ah, Bh, k, np.finfo(np.float64).eps) <= 10, alg
 
 
-def test_gpu_el_api_cpp(tmp_path):
+def test_gpu_el_api_cpp():
     """The drop-in C++ header on Device::GPU matrices (tests/cpp/test_el_api.cpp
     built with -DEL_TEST_GPU): Gemm, Matrix<T,GPU>/LockedMatrix Gemm, Syrk/Herk,
     Trsm (+ checkIfSingular), redistributions, Get/Set, Fill, level-1, Attach,
     Write/Read."""
+    _run_prebuilt("test_el_api_gpu")
+
+
+def _run_prebuilt(name: str):
+    """Run a C++ program __graft_entry__.build() compiled into tests/cpp/_build."""
     import os
-    import shutil
     import subprocess
-    from elemental_amd import _lib as L
-    gxx = shutil.which("g++")
-    if gxx is None:
-        pytest.skip("no g++")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = tmp_path / "test_el_api_gpu"
-    libdir = os.path.dirname(L.LIB_PATH)
-    subprocess.check_call([gxx, "-std=c++17", "-O1", "-DEL_TEST_GPU", "-I", os.path.join(root, "include"),
-                           os.path.join(root, "tests", "cpp", "test_el_api.cpp"), "-o", str(exe), "-L", libdir,
-                           "-lelemental_amd", f"-Wl,-rpath,{libdir}"])
-    res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "_build", name)
+    assert os.path.exists(exe), f"{exe} missing: run __graft_entry__.build()"
+    res = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "OK" in res.stdout
+
+
+def test_gpu_entrywise_functor():
+    """Functor-generic El::EntrywiseMap / El::Combine (include/El/EntrywiseMap.hip.hpp,
+    the reference's EntrywiseMapImpl / CombineImpl device templates) with user
+    device lambdas and a functor struct, compiled by hipcc as a caller would."""
+    _run_prebuilt("test_entrywise_functor")
 
 
 def test_gpu_summa_pipeline_multi_panel():
