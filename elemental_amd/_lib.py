@@ -45,6 +45,8 @@ _SIGS = {
     "elx_get_device": (_i, [POINTER(c_int)]),
     "elx_device_synchronize": (_i, []),
     "elx_default_stream": (_i, [POINTER(c_void_p)]),
+    "elx_comm_stream": (_i, [POINTER(c_void_p)]),
+    "elx_reserved_cus": (_i, [POINTER(c_int)]),
     "elx_stream_create": (_i, [POINTER(c_void_p)]),
     "elx_stream_destroy": (_i, [_vp]),
     "elx_stream_synchronize": (_i, [_vp]),

@@ -60,6 +60,8 @@ int elx_device_synchronize(void) {
     return Guard([&] { Runtime::Get().EnsureGPU(); ELX_CHECK_HIP(hipDeviceSynchronize()); });
 }
 int elx_default_stream(void** stream) { return Guard([&] { *stream = Runtime::Get().ComputeStream(); }); }
+int elx_comm_stream(void** stream) { return Guard([&] { *stream = Runtime::Get().CommStream(); }); }
+int elx_reserved_cus(int* cus) { return Guard([&] { *cus = Runtime::Get().ReservedCUs(); }); }
 int elx_stream_create(void** stream) {
     return Guard([&] {
         Runtime::Get().EnsureGPU();

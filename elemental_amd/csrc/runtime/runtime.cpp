@@ -1,6 +1,8 @@
 #include "runtime.hpp"
+#include <algorithm>
 #include <cstdlib>
 #include <limits>
+#include <vector>
 
 namespace elx {
 
@@ -39,7 +41,26 @@ void Runtime::EnsureGPU() {
     if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
         throw NoDeviceError(Cat("elx: device ", device_, " is ", prop.gcnArchName,
                                 "; this build targets gfx950 (MI355X) only"));
-    ELX_CHECK_HIP(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+    // ELX_COMM_CUS = R > 0: the compute stream (the MFMA panel updates) is
+    // masked off R CUs so the comm stream's pack/unpack and RCCL kernels always
+    // find free CUs while a full-machine GEMM grid is resident.  The reserved CUs
+    // are spread so that both a blocked (i / 32) and an interleaved (i % 8)
+    // CU-to-XCD numbering put them on different XCDs.
+    const int ncu = prop.multiProcessorCount;
+    if (const char* e = std::getenv("ELX_COMM_CUS")) reserved_cus_ = std::max(0, std::atoi(e));
+    if (reserved_cus_ > 0 && reserved_cus_ < ncu) {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+        for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+        const int slice = ncu / reserved_cus_;
+        for (int r = 0; r < reserved_cus_; ++r) {
+            const int i = std::min(ncu - 1, r * slice + (r % 8) % std::max(1, slice));
+            mask[i / 32] &= ~(1u << (i % 32));
+        }
+        ELX_CHECK_HIP(hipExtStreamCreateWithCUMask(&compute_, static_cast<uint32_t>(mask.size()), mask.data()));
+    } else {
+        reserved_cus_ = 0;
+        ELX_CHECK_HIP(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+    }
     int lo = 0, hi = 0;
     ELX_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     // communication gets the higher priority so panel broadcasts are not

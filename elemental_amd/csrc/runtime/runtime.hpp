@@ -22,6 +22,8 @@ public:
     hipStream_t ComputeStream() { EnsureGPU(); return compute_; }
     hipStream_t CommStream() { EnsureGPU(); return comm_; }
     hipStream_t Resolve(void* s) { return s ? static_cast<hipStream_t>(s) : ComputeStream(); }
+    // CUs masked off the compute stream for communication kernels (ELX_COMM_CUS)
+    int ReservedCUs() { EnsureGPU(); return reserved_cus_; }
 
     // Stream-ordered pool allocation (hipMallocFromPoolAsync / hipFreeAsync).
     void* Alloc(size_t bytes, hipStream_t s);
@@ -34,6 +36,7 @@ private:
     std::mutex mu_;
     bool gpu_ready_ = false;
     int device_ = -1;
+    int reserved_cus_ = 0;
     hipStream_t compute_ = nullptr, comm_ = nullptr;
     hipMemPool_t pool_ = nullptr;
     std::unordered_map<void*, size_t> live_;

@@ -106,6 +106,11 @@ int elx_get_device(int* device);
 int elx_device_synchronize(void);
 /* replaces SyncInfo<Device::GPU> {stream, event} (include/hydrogen/device/gpu/rocm/SyncInfo.hpp:15-41) */
 int elx_default_stream(void** stream);
+/* the high-priority stream the SUMMA drivers move panels on */
+int elx_comm_stream(void** stream);
+/* CUs masked off the compute stream for communication kernels (env ELX_COMM_CUS,
+ * read at device initialisation; 0 = none) */
+int elx_reserved_cus(int* cus);
 int elx_stream_create(void** stream);
 int elx_stream_destroy(void* stream);
 int elx_stream_synchronize(void* stream);
