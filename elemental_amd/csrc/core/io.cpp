@@ -109,14 +109,25 @@ void Read(DistMatrix& A, const std::string& filename, int format, int intBytes) 
     if (bytes != expect) throw RuntimeError(Cat("Expected file to be ", expect, " bytes but found ", bytes));
     DistMatrix R(A.GridPtr(), A.Type(), Dist::CIRC, Dist::CIRC, A.G().CommDevice(), 0);
     R.Resize(m, n);
+    // only the root reads the body: its success is broadcast before the
+    // collective scatter, so a failure raises on every rank instead of leaving
+    // the others waiting in the redistribution
+    std::string err;
     if (A.G().VCRank() == 0 && m > 0 && n > 0) {
-        std::vector<unsigned char> data(static_cast<size_t>(m * n) * FileElem(A.Type()));
-        if (std::fread(data.data(), 1, data.size(), file.f) != data.size())
-            throw RuntimeError(Cat("short read from ", filename));
-        std::vector<unsigned char> local(static_cast<size_t>(m * n) * A.ElemSize());
-        FromFile(A.Type(), data.data(), local.data(), static_cast<size_t>(m * n));
-        R.SetLocal(local.data(), m);
+        try {
+            std::vector<unsigned char> data(static_cast<size_t>(m * n) * FileElem(A.Type()));
+            if (std::fread(data.data(), 1, data.size(), file.f) != data.size())
+                throw RuntimeError(Cat("short read from ", filename));
+            std::vector<unsigned char> local(static_cast<size_t>(m * n) * A.ElemSize());
+            FromFile(A.Type(), data.data(), local.data(), static_cast<size_t>(m * n));
+            R.SetLocal(local.data(), m);
+        } catch (const std::exception& e) {
+            err = e.what();
+            if (err.empty()) err = "read failed";
+        }
     }
+    if (GridBcast(A.G(), err.empty() ? 1.0 : 0.0, 0) == 0.0)
+        throw RuntimeError(err.empty() ? Cat("short read from ", filename, " on the root rank") : err);
     Copy(R, A);
 }
 

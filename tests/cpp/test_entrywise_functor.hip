@@ -19,6 +19,10 @@ static int failures = 0;
         }                                                                                   \
     } while (0)
 
+// the device may contract a*b+c into one fused multiply-add (one rounding where
+// the host rounds twice): compare to a few ulps
+static bool Near(double got, double want) { return std::fabs(got - want) <= 4e-16 * (std::fabs(want) + 1.0); }
+
 struct LeakyRelu {  // a functor type with state
     float slope;
     __host__ __device__ float operator()(float x) const { return x > 0.f ? x : slope * x; }
@@ -43,13 +47,13 @@ int main() {
     // a device lambda on local matrices: an owned Matrix<double,GPU> is resized to A's block
     El::Matrix<double, El::Device::GPU> Bm;
     El::EntrywiseMap(A.LockedMatrix(), Bm, [] __device__(double x) { return 3.0 * x * x - 1.0; });
-    EXPECT(Bm.Height() == m && Bm.Width() == n && Bm.Get(7, 3) == 3.0 * a[7 + 3 * m] * a[7 + 3 * m] - 1.0);
+    EXPECT(Bm.Height() == m && Bm.Width() == n && Near(Bm.Get(7, 3), 3.0 * a[7 + 3 * m] * a[7 + 3 * m] - 1.0));
     (void)B;
     GPUMat B2(m, n, g);
     El::EntrywiseMap(A, B2, [] __device__(double x) { return 3.0 * x * x - 1.0; });
     auto b = Local(B2);
     bool ok = true;
-    for (Int i = 0; i < m * n; ++i) ok &= b[i] == 3.0 * a[i] * a[i] - 1.0;
+    for (Int i = 0; i < m * n; ++i) ok &= Near(b[i], 3.0 * a[i] * a[i] - 1.0);
     EXPECT(ok);
 
     // Combine: B2 := a * B2 + 1 (binary lambda), then in place B2 := -B2
@@ -57,7 +61,7 @@ int main() {
     El::EntrywiseMap(B2, [] __host__ __device__(double y) { return -y; });
     b = Local(B2);
     ok = true;
-    for (Int i = 0; i < m * n; ++i) ok &= b[i] == -(a[i] * (3.0 * a[i] * a[i] - 1.0) + 1.0);
+    for (Int i = 0; i < m * n; ++i) ok &= Near(b[i], -(a[i] * (3.0 * a[i] * a[i] - 1.0) + 1.0));
     EXPECT(ok);
 
     // type-changing map with a functor struct: double [MC,MR] -> float [STAR,VR]
