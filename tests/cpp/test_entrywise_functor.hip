@@ -77,11 +77,13 @@ int main() {
         ok &= f[i] == LeakyRelu{0.25f}(static_cast<float>(as[i]));
     EXPECT(ok);
 
-    // Matrix<T,GPU> directly, with a caller stream
-    El::Matrix<float, El::Device::GPU> X(300, 5), Y;
-    El::Fill(X, 2.0f);
+    // Matrix<T,GPU> directly, with a caller stream (created before and destroyed
+    // after the matrices that use it: Y's buffer is released on it)
     void* s = nullptr;
     elx_stream_create(&s);
+    {
+    El::Matrix<float, El::Device::GPU> X(300, 5), Y;
+    El::Fill(X, 2.0f);
     Y.SetStream(s);
     El::EntrywiseMap(X, Y, LeakyRelu{0.5f});
     El::Combine(X, Y, [] __device__(float x, float y) { return x - 4.f * y; });  // 2 - 8 = -6
@@ -95,6 +97,7 @@ int main() {
         threw = true;
     }
     EXPECT(threw);
+    }
     (void)hipDeviceSynchronize();
     elx_stream_destroy(s);
     if (failures) {
@@ -102,5 +105,6 @@ int main() {
         return 1;
     }
     std::printf("functor EntrywiseMap/Combine test OK\n");
+    std::fflush(stdout);
     return 0;
 }

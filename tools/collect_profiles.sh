@@ -5,7 +5,7 @@
 TAG=${1:-r01}; shift
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-c3-1gpu $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG} -o bench -- python3 $R/bench.py $ARGS > $R/gpurun_out/prof_${TAG}_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; case $rc in 124|137|134|139) exit $rc;; esac
 i=0
