@@ -359,6 +359,24 @@ def main():
             ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
                         "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
         out["entrywise"] = ew
+    if config == "c4":
+        # the same product with [MC,MR] inputs: SUMMA_DOT's read
+        # proxies first redistribute A and B to [VC,*] (TN.hpp:384-391), inside
+        # the timed region
+        del A, B
+        Am = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
+        Bm = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
+        el.Gemm(oA, el.NORMAL, 0.5, Am, Bm, -0.5, C)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            el.Gemm(oA, el.NORMAL, 0.5, Am, Bm, -0.5, C)
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t1)
+        out["c4_mcmr_inputs"] = {"workload": workload.replace("[VC,STAR]", "[MC,MR] (proxied to [VC,STAR] each call)"),
+                                 "value": round(2.0 * m * n * k * args.steps / dt / 1e12, 3), "unit": "TFLOP/s",
+                                 "ms_per_step": round(dt / args.steps * 1e3, 3)}
+        del Am, Bm
     if world == 1 and config == "c2" and not args.n and not args.no_c3_1gpu:
         # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 4096
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU

@@ -391,6 +391,115 @@ __global__ __launch_bounds__(NT, 1) void gemm_h8p_kernel(H2Params p) {
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
+// ---------------------------------------------------------------------------
+// Balanced-read variant of the phased kernel: the same tile, images, quadrant
+// order and barrier schedule, but the next K-tile's images are staged in the
+// order B0, A0, B1, A1 and B0(t+1) is read in phase 3 of K-tile t (into the B
+// register set B1(t) just vacated), so the fragment reads per phase are
+// 8, 4, 8, 4 instead of 12, 4, 8, 0 (the 12-read phase 0 is as long in LDS
+// cycles as its 16 MFMAs).  The two B register sets swap roles every K-tile
+// (the loop is unrolled by two).  Every phase waits vmcnt(4): the image read
+// in the next phase was staged two phases earlier (RAW), and every image is
+// restaged >= 4 phases after its last read (WAR).
+// ---------------------------------------------------------------------------
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__device__ __forceinline__ void step8b(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
+                                       const lds_char* __restrict__ cur, f32x4 (&acc)[8][4], u32x4 (&a)[8],
+                                       u32x4 (&bY)[4], u32x4 (&bX)[4]) {
+    const int ar = f.wr * 64, bcol = f.wc * 32;
+    auto load_a = [&](const lds_char* img) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) a[s * 4 + mi] = frag<KCA>(img, ar + mi * 16, s, f.l);
+    };
+    auto load_b = [&](u32x4 (&b)[4], const lds_char* img) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b[s * 2 + ni] = frag<KCB>(img, bcol + ni * 16, s, f.l);
+    };
+    auto wait = [&]() {
+        if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    // phase 0: quadrant (0,0): A0(t) read now, B0(t) already in bY
+    load_a(cur);
+    if (more) stage_q<BUF, KCB>(f, 2, knext, next + 2 * HALF);
+    wait();
+    bar8();
+    cluster<BF16>(acc, 0, 0, a, bY);
+    bar8();
+    // phase 1: quadrant (0,1) from B1(t)
+    load_b(bX, cur + 3 * HALF);
+    if (more) stage_q<BUF, KCA>(f, 0, knext, next);
+    wait();
+    bar8();
+    cluster<BF16>(acc, 0, 1, a, bX);
+    bar8();
+    // phase 2: quadrant (1,1) from A1(t)
+    load_a(cur + HALF);
+    if (more) stage_q<BUF, KCB>(f, 3, knext, next + 3 * HALF);
+    wait();
+    bar8();
+    cluster<BF16>(acc, 1, 1, a, bX);
+    bar8();
+    // phase 3: quadrant (1,0) from registers; B0(t+1) (waited in phase 2) read into bX
+    if (more) {
+        load_b(bX, next + 2 * HALF);
+        stage_q<BUF, KCA>(f, 1, knext, next + HALF);
+    }
+    wait();
+    bar8();
+    cluster<BF16>(acc, 1, 0, a, bY);
+    bar8();
+}
+
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__global__ __launch_bounds__(NT, 1) void gemm_h8b_kernel(H2Params p) {
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    stage_q<BUF, KCB>(f, 2, 0, lds + 2 * HALF);
+    stage_q<BUF, KCA>(f, 0, 0, lds);
+    stage_q<BUF, KCB>(f, 3, 0, lds + 3 * HALF);
+    stage_q<BUF, KCA>(f, 1, 0, lds + HALF);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar8();
+    u32x4 a[8], b0[4], b1[4];
+    {
+        const int bcol = wc * 32;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b0[s * 2 + ni] = frag<KCB>(lds + 2 * HALF, bcol + ni * 16, s, l);
+    }
+    if (wr == 1) bar8();  // group 1 runs one barrier behind group 0
+    for (int t = 0; t < nt; t += 2) {
+        step8b<BF16, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + STAGE, lds, acc, a, b0, b1);
+        if (t + 1 < nt)
+            step8b<BF16, KCA, KCB, BUF>(f, (i64)(t + 2) * BK, t + 2 < nt, lds, lds + STAGE, acc, a, b1, b0);
+    }
+    if (wr == 0) bar8();  // matches group 1's last barrier
+
+    epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
+}
+
 // C = alpha acc + beta C.  C/D map of 16x16x32: col = lane&15, rows 4*(lane>>4) + r
 // (r = 0..3), i.e. four consecutive rows of one column = one 8-B access per tile.
 template <bool BF16>
@@ -449,13 +558,22 @@ hipError_t launch_p(const H2Params& p, hipStream_t s, int fl) {
     return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF>, p, s);
 }
 
-// Default: the phased kernel.  ELX_H16_KERNEL=s selects the two-stage kernel;
+// Kernel choice (launch_h256): balanced-read (default), phased (ELX_H16_KERNEL=p), two-stage (=s);
 // ELX_H16_FLAGS picks a timing ablation (profiles/r01_h16_ablation.log) of the
 // two-stage bf16 NN or phased bf16 TN kernel.
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h256(const H2Params& p, hipStream_t s) {
     static const int fl = [] { const char* v = getenv("ELX_H16_FLAGS"); return v ? atoi(v) : 0; }();
     static const bool two_stage = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 's'; }();
+    // default: the balanced-read kernel (+2-5 % over the phased kernel at 16384^3,
+    // profiles/r02_h16_experiments.log); ELX_H16_KERNEL=p the phased kernel (and
+    // its ablations), =s the two-stage kernel
+    static const bool balanced = [] { const char* v = getenv("ELX_H16_KERNEL"); return !v || v[0] == 'b'; }();
+    if (balanced && fl == 0) {
+        if (dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2))
+            return launch(gemm_h8b_kernel<BF16, KCA, KCB, true>, p, s);
+        return launch(gemm_h8b_kernel<BF16, KCA, KCB, false>, p, s);
+    }
     if (two_stage) {
         if constexpr (BF16 && !KCA && KCB) {
             if (fl == 1) return launch(gemm_h256_kernel<BF16, KCA, KCB, 1>, p, s);
