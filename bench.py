@@ -47,25 +47,13 @@ KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_f32g_kernel (LDS-DMA
 
 
 def cpu_baseline(seconds_target: float = 10.0) -> dict:
-    """The CPU leg (oracle/cpu_gemm.c: blocked, packed, OpenMP f64 GEMM standing
-    in for the reference's multi-threaded BLAS dgemm of its CPU path) on the
-    host's cores, on a bounded sample of the same workload: NN fp64 s x s x s
-    with the same input distribution, repeated for ~seconds_target."""
-    import oracle
-    s = 4096
-    A = oracle.hash_matrix(s, s, 1, 0.0, 0.1)
-    B = oracle.hash_matrix(s, s, 2, 0.0, 0.1)
-    C = oracle.hash_matrix(s, s, 3, 0.0, 0.1)
-    oracle.cpu_gemm("N", "N", 0.5, A, B, -0.5, C)  # warm-up (thread pool, pages)
-    reps, total = 0, 0.0
-    while total < seconds_target:
-        t0 = time.perf_counter()
-        oracle.cpu_gemm("N", "N", 0.5, A, B, -0.5, C)
-        total += time.perf_counter() - t0
-        reps += 1
-    cores = oracle.cpu_threads()
-    return {"value": round(2.0 * s ** 3 * reps / total / 1e12, 4), "unit": "TFLOP/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/cpu_gemm.c blocked OpenMP dgemm NN fp64 {s}^3 x{reps}, {cores} threads, {total:.1f} s"}
+    """The CPU leg (BASELINE.md §3): C1 (BASELINE.json configs[0]), El::Gemm NN
+    fp64 4096^3 on a 2x2 grid, run as the reference's CPU path runs it: SUMMA_NNC
+    over 4 processes with nb = 128 all-gathers (gloo) and a blocked OpenMP dgemm
+    for the local updates (oracle/cpu_summa.py over oracle/cpu_gemm.c, the port
+    of the reference's BLAS call), on the box's cores, for ~seconds_target."""
+    from oracle import cpu_summa
+    return cpu_summa.run(n=4096, nb=128, r=2, c=2, seconds=seconds_target)
 
 
 def measured_traffic(dtype: str, n: int, world: int):

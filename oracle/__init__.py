@@ -71,6 +71,8 @@ def lib():
                                        c_void_p, i64]
         L.orc_cpu_threads.restype = c_int
         L.orc_cpu_threads.argtypes = []
+        L.orc_cpu_set_threads.restype = None
+        L.orc_cpu_set_threads.argtypes = [c_int]
         _lib = L
     return _lib
 

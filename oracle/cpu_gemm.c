@@ -116,3 +116,13 @@ int orc_cpu_threads(void) {
     return 1;
 #endif
 }
+
+/* threads of this process's later parallel regions (OMP_NUM_THREADS is read
+ * once, when the OpenMP runtime loads, possibly before the caller could set it) */
+void orc_cpu_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

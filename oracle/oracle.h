@@ -59,6 +59,7 @@ void orc_summa_nnc_f64(int r, int c, int64_t m, int64_t n, int64_t k, int64_t nb
 void orc_cpu_gemm_f64(char ta, char tb, int64_t m, int64_t n, int64_t k, double alpha, const double* A, int64_t lda,
                       const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
 int orc_cpu_threads(void);
+void orc_cpu_set_threads(int n);
 
 /* parity metric of the north_star: ||C - Cref||_F / (||A||_F ||B||_F k eps) */
 double orc_fro(int64_t m, int64_t n, const double* X, int64_t ldx);
