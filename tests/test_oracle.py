@@ -172,3 +172,11 @@ def test_convert_restatement_known_answers():
     assert [int(x) for x in got] == list(ka.values())
     # f64 -> bf16 via f32 would round 1 + 2^-8 + 2^-30 to the tie 1 + 2^-8 and then to 1.0
     assert int(oracle.f32_to_bf16_bits(np.array([1 + 2.0 ** -8 + 2.0 ** -30], dtype=np.float32))[0]) == 0x3F80
+
+
+def test_cpu_summa_baseline_small():
+    """bench.py's cpu_baseline leg (oracle/cpu_summa.py): the C1-shaped CPU SUMMA
+    on a 2x2 grid of gloo processes runs and its entry checks pass (small size)."""
+    from oracle import cpu_summa
+    res = cpu_summa.run(n=256, nb=16, kc=64, r=2, c=2, seconds=0.2, cores=4)
+    assert res["value"] > 0 and res["kind"] == "port" and res["cores"] == 4
