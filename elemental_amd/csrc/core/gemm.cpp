@@ -981,11 +981,10 @@ void Syr2k(int uplo, int orient, double alpha, const DistMatrix& A, const DistMa
 //   op(A) panel gathered [MC,*] / [*,MC], X1 as [*,MR], MFMA update).
 // RIGHT solves the transposed LEFT problem (X op(A) = B <=> op(A)^T X^T = B^T)
 // through two distributed transposes.  f64/f32 (the reference's GPU Trsm types).
-Int TrsmOuter() {  // ELX_TRSM_OUTER overrides (tests: several outer blocks at small sizes)
-    static const Int v = [] {
-        const char* e = getenv("ELX_TRSM_OUTER");
-        return e && atoll(e) > 0 ? (Int)atoll(e) : Int(1024);
-    }();
+// ELX_TRSM_FLAT=1: the reference's flat nb-step sweep (every update k = nb over
+// all remaining rows) instead of the recursive split (tests, ablation)
+bool TrsmFlat() {
+    static const bool v = [] { const char* e = getenv("ELX_TRSM_FLAT"); return e && atoi(e) > 0; }();
     return v;
 }
 
@@ -1001,75 +1000,100 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     auto A11s = A.Like(Dist::STAR, Dist::STAR);
     auto X1v = X.Like(Dist::STAR, Dist::VR);
     // X_rest -= op(A)(r0:r1, k0:k1) X(k0:k1, :) through the SUMMA pipeline on views
+    // (solved rows are read from `src`: X itself, or Y on the batched path)
+    const DistMatrix* src = &X;
     auto update = [&](Int r0, Int r1, Int k0, Int k1) {
-        if (r1 <= r0 || n == 0) return;
+        if (r1 <= r0 || k1 <= k0 || n == 0) return;
         auto Ar = trans ? DistMatrix::View(A, k0, k1, r0, r1) : DistMatrix::View(A, r0, r1, k0, k1);
-        auto Xk = DistMatrix::View(X, k0, k1, 0, n);
+        auto Xk = DistMatrix::View(*src, k0, k1, 0, n);
         auto Xr = DistMatrix::View(X, r0, r1, 0, n);
         SummaC(trans ? ELX_TRANSPOSE : ELX_NORMAL, ELX_NORMAL, -1.0, *Ar, *Xk, 1.0, *Xr);
     };
-    // Two levels: outer blocks of TrsmOuter() (1024) rows (whole nb blocks) carry the
-    // trailing update as one deep (k = outer) MFMA GEMM; inside an outer block
-    // the reference's nb-step runs (Trsm/LLN.hpp:40-70) with updates confined to
-    // it.  Same eliminations, fewer and deeper launches than k = nb updates.
     // A whose local block is the whole matrix (1x1 grid): every diagonal block's
     // inverse comes from ONE batched launch up front (the per-block inversions
-    // are independent), applied per block as an MFMA GEMM; elsewhere each block
-    // is solved where it lands (exec::Trsm)
+    // are independent), applied per block as an MFMA GEMM whose output goes
+    // straight into a second buffer Y (no write-back per block; every later
+    // update reads solved rows from Y, copied into X once at the end);
+    // elsewhere each block is solved where it lands (exec::Trsm)
     const size_t es = DTypeSize(X.Type());
     Buffer winv;
     const bool batched = X.Dev() == Device::GPU && SameLocalLayout(A, Dist::STAR, Dist::STAR, 0, 0) &&
                          nb * 65 * (Int)es <= 66 * 1024 && (m + nb - 1) / nb <= 65535 &&
                          SameLocalLayout(X, Dist::STAR, Dist::VR, 0, X.RowAlign()) && X.LocalWidth() >= 4 * nb;
+    std::shared_ptr<DistMatrix> Y;
     if (batched) {
         FenceStreams(A.Stream(), X.Stream());
         winv.Reset(Device::GPU, static_cast<size_t>((m + nb - 1) / nb) * nb * nb * es, X.Stream());
         exec::TriInverseBatched(X.Type(), lower, trans, unit, nb, m, A.Buffer(), A.LDim(), winv.data(), X.Stream());
+        Y = X.Like(Dist::MC, Dist::MR);
+        Y->Align(X.ColAlign(), X.RowAlign(), true);
+        Y->Resize(m, n);
+        src = Y.get();
     }
-    const Int ob = std::max<Int>(nb, (TrsmOuter() + nb - 1) / nb * nb);
-    const Int nouter = (m + ob - 1) / ob;
-    for (Int oi = 0; oi < nouter; ++oi) {
-        const Int o = forward ? oi : nouter - 1 - oi;
-        const Int K0 = o * ob, K1 = std::min(m, K0 + ob);
-        const Int nblk = (K1 - K0 + nb - 1) / nb;
+    // X(k0:k1, :) := op(A11)^-1 X(k0:k1, :), one nb block (Trsm/LLN.hpp:49-60)
+    auto leaf = [&](Int k0, Int k1) {
+        auto X1 = DistMatrix::View(X, k0, k1, 0, n);
+        if (batched) {
+            auto Y1 = DistMatrix::View(*Y, k0, k1, 0, n);
+            exec::Gemm(X.Dev(), X.Type(), false, false, k1 - k0, X1->LocalWidth(), k1 - k0, 1.0,
+                       static_cast<const char*>(winv.data()) + (k0 / nb) * nb * nb * es, nb, X1->Buffer(),
+                       X1->LDim(), 0.0, Y1->Buffer(), Y1->LDim(), X1->Stream());
+            return;
+        }
+        // a block whose local storage already IS the [*,*] / [*,VR] layout (a
+        // 1x1 grid) is used in place: no redistribution temporaries
+        auto A11 = DistMatrix::View(A, k0, k1, k0, k1);
+        std::shared_ptr<const DistMatrix> a11 = A11;
+        if (!SameLocalLayout(*A11, Dist::STAR, Dist::STAR, 0, 0)) {
+            Copy(*A11, *A11s);                               // A11[*,*] <- A11[MC,MR]
+            a11 = A11s;
+        }
+        const bool inplace = SameLocalLayout(*X1, Dist::STAR, Dist::VR, 0, X1->RowAlign());
+        DistMatrix* x1 = X1.get();
+        if (!inplace) {
+            X1v->AlignRows(X.RowAlign(), true);
+            Copy(*X1, *X1v);                                 // X1[*,VR] <- X1[MC,MR]
+            x1 = X1v.get();
+        }
+        if (X.Dev() == Device::GPU) FenceStreams(a11->Stream(), x1->Stream());
+        exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, x1->LocalWidth(), a11->Buffer(), a11->LDim(),
+                   x1->Buffer(), x1->LDim(), x1->Stream());
+        if (!inplace) Copy(*X1v, *X1);                       // X1[MC,MR] <- X1[*,VR]
+    };
+    const Int nblk = (m + nb - 1) / nb;
+    if (TrsmFlat()) {
+        // the reference's order (Trsm/LLN.hpp:40-70): solve block b, then update
+        // every remaining row with k = nb
         for (Int bi = 0; bi < nblk; ++bi) {
             const Int b = forward ? bi : nblk - 1 - bi;
-            const Int k0 = K0 + b * nb, k1 = std::min(K1, k0 + nb);
-            if (batched) {
-                auto X1 = DistMatrix::View(X, k0, k1, 0, n);
-                exec::ApplyInverse(X.Dev(), X.Type(), k1 - k0, X1->LocalWidth(),
-                                   static_cast<const char*>(winv.data()) + (k0 / nb) * nb * nb * es, nb, X1->Buffer(),
-                                   X1->LDim(), X1->Stream());
-                if (forward) update(k1, K1, k0, k1);
-                else update(K0, k0, k0, k1);
-                continue;
-            }
-            // a block whose local storage already IS the [*,*] / [*,VR] layout (a
-            // 1x1 grid) is used in place: no redistribution temporaries
-            auto A11 = DistMatrix::View(A, k0, k1, k0, k1);
-            std::shared_ptr<const DistMatrix> a11 = A11;
-            if (!SameLocalLayout(*A11, Dist::STAR, Dist::STAR, 0, 0)) {
-                Copy(*A11, *A11s);                               // A11[*,*] <- A11[MC,MR]
-                a11 = A11s;
-            }
-            auto X1 = DistMatrix::View(X, k0, k1, 0, n);
-            const bool inplace = SameLocalLayout(*X1, Dist::STAR, Dist::VR, 0, X1->RowAlign());
-            DistMatrix* x1 = X1.get();
-            if (!inplace) {
-                X1v->AlignRows(X.RowAlign(), true);
-                Copy(*X1, *X1v);                                 // X1[*,VR] <- X1[MC,MR]
-                x1 = X1v.get();
-            }
-            if (X.Dev() == Device::GPU) FenceStreams(a11->Stream(), x1->Stream());
-            exec::Trsm(X.Dev(), X.Type(), lower, trans, unit, k1 - k0, x1->LocalWidth(), a11->Buffer(), a11->LDim(),
-                       x1->Buffer(), x1->LDim(), x1->Stream());
-            if (!inplace) Copy(*X1v, *X1);                       // X1[MC,MR] <- X1[*,VR]
-            if (forward) update(k1, K1, k0, k1);
-            else update(K0, k0, k0, k1);
+            const Int k0 = b * nb, k1 = std::min(m, k0 + nb);
+            leaf(k0, k1);
+            if (forward) update(k1, m, k0, k1);
+            else update(0, k0, k0, k1);
         }
-        if (forward) update(K1, m, K0, K1);
-        else update(0, K0, K0, K1);
+    } else {
+        // Recursive split at a block boundary: solve the half op(A) reaches first,
+        // eliminate it from the other half with ONE GEMM (k = that half's height),
+        // solve the other half.  The same eliminations as the nb-step sweep, but
+        // half of all update FLOPs go to a k = m/2 GEMM, a quarter to two k = m/4
+        // ones, ...: deep, full-machine MFMA launches instead of m/nb k = nb ones.
+        std::function<void(Int, Int)> solve = [&](Int K0, Int K1) {
+            const Int nbk = (K1 - K0 + nb - 1) / nb;
+            if (nbk <= 1) return leaf(K0, K1);
+            const Int mid = K0 + (nbk / 2) * nb;
+            if (forward) {
+                solve(K0, mid);
+                update(mid, K1, K0, mid);
+                solve(mid, K1);
+            } else {
+                solve(mid, K1);
+                update(K0, mid, mid, K1);
+                solve(K0, mid);
+            }
+        };
+        if (m > 0) solve(0, m);
     }
+    if (Y) Copy(*Y, X);
     Xp.Finish();
 }
 

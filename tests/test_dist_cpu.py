@@ -102,13 +102,13 @@ def test_syrk_herk(world, height, cols, monkeypatch):
     _spawn(W.syrk_worker, world, height, el.CPU, el.F64, [(23, 9), (7, 30)], 4, 17)
 
 
-@pytest.mark.parametrize("world,height,outer", [(1, 1, 0), (2, 1, 0), (2, 2, 0), (4, 2, 0), (1, 1, 8),
-                                                (4, 2, 5)])
-def test_trsm(world, height, outer, monkeypatch):
-    """El::Trsm LEFT/RIGHT x LOWER/UPPER x N/T x NON_UNIT/UNIT, ragged blocks (nb = 4);
-    outer > 0: several outer blocks (deep trailing updates) at this small size."""
-    if outer:
-        monkeypatch.setenv("ELX_TRSM_OUTER", str(outer))
+@pytest.mark.parametrize("world,height,flat", [(1, 1, 0), (2, 1, 0), (2, 2, 0), (4, 2, 0), (1, 1, 1),
+                                               (4, 2, 1)])
+def test_trsm(world, height, flat, monkeypatch):
+    """El::Trsm LEFT/RIGHT x LOWER/UPPER x N/T x NON_UNIT/UNIT, ragged blocks (nb = 4):
+    the recursive split (deep updates), and flat = 1 the reference's nb-step sweep."""
+    if flat:
+        monkeypatch.setenv("ELX_TRSM_FLAT", "1")
     _spawn(W.trsm_worker, world, height, el.CPU, el.F64, 19, 13, 4, 31)
 
 

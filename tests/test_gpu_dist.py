@@ -330,12 +330,13 @@ def test_gpu_syrk_large(dtype):
             assert num <= 10 * den, (uplo, orient, num / den)
 
 
-@pytest.mark.parametrize("world,height,outer", [(1, 1, 0), (2, 1, 0), (4, 2, 32)])
-def test_gpu_trsm_distributed(world, height, outer, monkeypatch):
+@pytest.mark.parametrize("world,height,flat", [(1, 1, 0), (2, 1, 0), (4, 2, 0), (4, 2, 1)])
+def test_gpu_trsm_distributed(world, height, flat, monkeypatch):
     """El::Trsm, all 16 side/uplo/orientation/diag cases, on the GPU (trsm_kernel +
-    the SUMMA trailing update), host-staged ranks on one device."""
-    if outer:
-        monkeypatch.setenv("ELX_TRSM_OUTER", str(outer))
+    the SUMMA trailing update), host-staged ranks on one device; flat = 1 the
+    reference's nb-step sweep instead of the recursive split."""
+    if flat:
+        monkeypatch.setenv("ELX_TRSM_FLAT", "1")
     _spawn(W.trsm_worker, world, height, el.GPU, el.F64, 45, 23, 16, 41)
 
 
