@@ -15,7 +15,8 @@ Default workload (the driver's line):
   N > 1 : C3, SUMMA El::Gemm NN fp64 m=n=k=65536 on Grid::DefaultHeight(N)
           (1x2, 2x2, 2x4): strong scaling of the same problem.
   N = 1 also reports "c3_1gpu": C3's n = 65536 on the one GPU through the same
-          kc = 4096 panel path, the same-problem denominator for strong scaling.
+          kc = 8192 panel path (the automatic panel at K = 65536 on grids
+          larger than 1x1), the same-problem denominator for strong scaling.
   N > 1 first checks the reference's associativity residual through the
           distributed path (n = 4096) and reports xGMI GB/s from transfer-only
           events plus the compute-stream gaps the panel pipeline left exposed.
@@ -132,7 +133,7 @@ def associativity_residual(el, grid, n: int = 4096, nrhs: int = 100) -> float:
 
 
 def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n: int = 65536,
-               kc: int = 4096) -> dict:
+               kc: int = 8192) -> dict:
     """C3 (El::Gemm NN fp64 m=n=k=65536) on a 1x1 grid through the panel path:
     k in kc-deep compute panels exactly as on the 1x2 / 2x2 / 2x4 grids (there the
     panels are gathered; here they are views), so value_N / (N * value) is a
@@ -366,7 +367,7 @@ def main():
                                  "ms_per_step": round(dt / args.steps * 1e3, 3)}
         del Am, Bm
     if world == 1 and config == "c2" and not args.n and not args.no_c3_1gpu:
-        # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 4096
+        # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 8192
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
         del A, B, C
         out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)

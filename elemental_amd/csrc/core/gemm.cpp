@@ -279,13 +279,13 @@ int TeamCount(const DistMatrix& C, Int panels) {
 Int EffectivePanel(const Grid& g, Int K, DType t) {
     const Int nb = std::max<Int>(1, g_blocksize);
     Int kc = g_compute_panel;
-    // automatic: C's HBM round trip per panel (16 B/element at fp64) against the
-    // panel's 2*kc FLOP/element stays ~2.5% of the MFMA time at kc = 4096
-    // (K = 65536 -> 16 panels); never below 2048, never above 8192.  16-bit
-    // MFMAs are 32x faster per element than fp64 for 1/4 of the C bytes, so
-    // they take panels twice as deep (K/8: 4096 at K = 32768).
-    const Int div = (t == DType::F16 || t == DType::BF16) ? 8 : 16;
-    if (kc <= 0) kc = (g.Size() == 1) ? K : std::min<Int>(8192, std::max<Int>(2048, K / div));
+    // automatic: K/8, never below 2048, never above 8192.  C's HBM round trip
+    // per panel (16 B/element at fp64) against the panel's 2*kc FLOP/element:
+    // C3 on one GPU (K = 65536) runs 72.9 TF at kc = 8192 vs 71.9 at 4096
+    // (profiles/r02_trsm_kc.log); the deeper first panel exposes ~4 ms more of
+    // transfer at 8 GPUs, against ~1 % of a ~1 s step.  16-bit MFMAs are 32x
+    // faster per element for 1/4 of the C bytes: K/8 is their floor as well.
+    if (kc <= 0) kc = (g.Size() == 1) ? K : std::min<Int>(8192, std::max<Int>(2048, K / 8));
     kc = std::max<Int>(nb, (kc + nb - 1) / nb * nb);  // whole communication panels
     return std::max<Int>(1, kc);
 }
