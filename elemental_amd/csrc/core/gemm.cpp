@@ -1002,8 +1002,19 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     // X_rest -= op(A)(r0:r1, k0:k1) X(k0:k1, :) through the SUMMA pipeline on views
     // (solved rows are read from `src`: X itself, or Y on the batched path)
     const DistMatrix* src = &X;
+    bool local = false;  // set on the batched path: every operand's local block is the whole matrix
     auto update = [&](Int r0, Int r1, Int k0, Int k1) {
         if (r1 <= r0 || k1 <= k0 || n == 0) return;
+        if (local) {  // one MFMA GEMM on the local blocks: no views, proxies or pipeline on the host
+            const size_t es = DTypeSize(X.Type());
+            const char* a = static_cast<const char*>(A.Buffer()) +
+                            ((trans ? k0 + r0 * A.LDim() : r0 + k0 * A.LDim()) * es);
+            const char* y = static_cast<const char*>(src->Buffer()) + k0 * es;
+            char* x = static_cast<char*>(X.Buffer()) + r0 * es;
+            exec::Gemm(X.Dev(), X.Type(), trans, false, r1 - r0, n, k1 - k0, -1.0, a, A.LDim(), y, src->LDim(), 1.0, x,
+                       X.LDim(), X.Stream());
+            return;
+        }
         auto Ar = trans ? DistMatrix::View(A, k0, k1, r0, r1) : DistMatrix::View(A, r0, r1, k0, k1);
         auto Xk = DistMatrix::View(*src, k0, k1, 0, n);
         auto Xr = DistMatrix::View(X, r0, r1, 0, n);
@@ -1029,6 +1040,7 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
         Y->Align(X.ColAlign(), X.RowAlign(), true);
         Y->Resize(m, n);
         src = Y.get();
+        local = X.LocalHeight() == m && X.LocalWidth() == n && Y->LDim() > 0 && !getenv("ELX_TRSM_SUMMA");
     }
     // X(k0:k1, :) := op(A11)^-1 X(k0:k1, :), one nb block (Trsm/LLN.hpp:49-60)
     auto leaf = [&](Int k0, Int k1) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace elx {
 namespace kern {
@@ -35,7 +36,14 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
     i64 z = (2 * slots + tiles - 1) / tiles;
     z = z < d.kmain / 2048 ? z : d.kmain / 2048;
     z = z < 16 ? z : 16;
-    if (z < 2) return d;
+    if (z < 2) {
+        // k too short to split: the DMA kernel on the few tiles there are, or
+        // (ELX_DMA_FEW=0) the register-staged kernel
+        static const bool few = [] { const char* v = getenv("ELX_DMA_FEW"); return !v || v[0] != '0'; }();
+        d.use = few && d.kmain > 0;
+        d.kchunk = d.kmain;
+        return d;
+    }
     d.use = true;
     d.kchunk = ((d.kmain + z - 1) / z + bk - 1) / bk * bk;
     d.nz = (int)((d.kmain + d.kchunk - 1) / d.kchunk);
