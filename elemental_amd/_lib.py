@@ -68,6 +68,13 @@ _SIGS = {
     "elx_matrix_copy": (_i, [_i, _i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_axpy2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_copy2d": (_i, [_i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
+    "elx_pack_strided": (_i, [_i, _i, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "elx_unpack_strided": (_i, [_i, _i, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "elx_pack_partial_strided": (_i, [_i, _i, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp,
+                                      _i64, _vp]),
+    "elx_unpack_partial_strided": (_i, [_i, _i, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
+                                        _vp, _i64, _vp]),
+    "elx_unpack_axpy_strided": (_i, [_i, _i, _i64, _i64, _d, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_copy2d_convert": (_i, [_i, _i, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "elx_transpose": (_i, [_i, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "elx_scale2d": (_i, [_i, _i64, _i64, _d, _vp, _i64, _vp]),
@@ -86,6 +93,11 @@ _SIGS = {
     "elx_comm_allgather": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
     "elx_comm_reduce_scatter": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
     "elx_comm_barrier": (_i, [_vp]),
+    "elx_comm_split": (_i, [_vp, _i, _i, POINTER(c_void_p)]),
+    "elx_comm_allreduce": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
+    "elx_comm_bcast": (_i, [_vp, _i, _vp, _i64, _i, _vp]),
+    "elx_comm_alltoall": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
+    "elx_comm_sendrecv": (_i, [_vp, _i, _vp, _i, _vp, _i, _i64, _vp]),
     "elx_comm_stats": (_i, [POINTER(c_int64), POINTER(c_double), POINTER(c_int64)]),
     "elx_comm_stats_reset": (_i, []),
     "elx_grid_default_height": (_i, [_i]),

@@ -210,6 +210,130 @@ int elx_copy2d_convert(int src_dtype, int dst_dtype, int64_t m, int64_t n, const
         exec::Convert2D(Device::GPU, ToDType(src_dtype), ToDType(dst_dtype), d, S(stream));
     });
 }
+// ---- pack / unpack for redistributions (Copy/util.hpp) ---------------------------
+// Each call is ONE batched strided-copy launch over all portions (the reference
+// issues one InterleaveMatrix per portion).  Portion k of a colStride-way split
+// holds the rows colShift(k) = Shift_(k, colAlign, colStride), colShift+colStride, ...
+// (indexing/impl.hpp:33-36,244-245), stored column-major with ld = its height.
+namespace {
+Device PackDev(int device) {
+    ELX_REQUIRE(device == ELX_DEVICE_CPU || device == ELX_DEVICE_GPU, "pack: bad device ", device);
+    return device == ELX_DEVICE_GPU ? Device::GPU : Device::CPU;
+}
+void RunCopies(int device, int dtype, const std::vector<kern::Copy2D>& d, bool axpy, double alpha, void* stream) {
+    if (d.empty()) return;
+    const Device dev = PackDev(device);
+    exec::Copy2DBatch(dev, ToDType(dtype), d.data(), (int)d.size(), axpy, alpha, dev == Device::GPU ? S(stream) : nullptr);
+}
+// StridedPack / StridedUnpack (util.hpp:667-718): portion k + l*colStride holds
+// the (colShift(k), rowShift(l)) sub-lattice; col/row-only forms are stride 1
+std::vector<kern::Copy2D> StridedPlan(int dtype, Int h, Int w, Int colAlign, Int colStride, Int rowAlign,
+                                      Int rowStride, const void* M, Int ldm, const void* P, Int portionSize,
+                                      bool pack) {
+    ELX_REQUIRE(h >= 0 && w >= 0 && colStride > 0 && rowStride > 0 && portionSize >= 0 && ldm >= std::max<Int>(1, h),
+                "pack: bad sizes");
+    const size_t es = DTypeSize(ToDType(dtype));
+    std::vector<kern::Copy2D> d;
+    for (Int l = 0; l < rowStride; ++l) {
+        const Int rs = Shift(l, rowAlign, rowStride), lw = Length(w, rs, rowStride);
+        for (Int k = 0; k < colStride; ++k) {
+            const Int cs = Shift(k, colAlign, colStride), lh = Length(h, cs, colStride);
+            ELX_REQUIRE(lh * lw <= portionSize, "pack: portion ", k + l * colStride, " needs ", lh * lw,
+                        " elements, portionSize is ", portionSize);
+            if (lh == 0 || lw == 0) continue;
+            char* m = (char*)M + (cs + rs * ldm) * es;
+            char* q = (char*)P + (k + l * colStride) * portionSize * es;
+            if (pack) d.push_back({lh, lw, m, colStride, rowStride * ldm, q, 1, lh});
+            else d.push_back({lh, lw, q, 1, lh, m, colStride, rowStride * ldm});
+        }
+    }
+    return d;
+}
+// PartialColStridedPack / Unpack (util.hpp:460-552) and the row forms
+// (:186-230, :308-355): portion k holds the rows of partial rank
+// colRankPart + k*colStridePart, read from a matrix whose own rows start at shift0
+// with stride colStridePart (so those rows sit colStrideUnion apart in it)
+std::vector<kern::Copy2D> PartialPlan(int dtype, bool cols, Int h, Int w, Int align, Int stride, Int strideUnion,
+                                      Int stridePart, Int rankPart, Int shift0, const void* M, Int ldm,
+                                      const void* P, Int portionSize, bool pack) {
+    // (cols: `height` is the global height and M holds the rows of the partial
+    // lattice from shift0, so its own height is Length_(h, shift0, stridePart))
+    ELX_REQUIRE(h >= 0 && w >= 0 && stride > 0 && strideUnion > 0 && stridePart > 0 && portionSize >= 0 &&
+                    ldm >= std::max<Int>(1, cols ? Length(h, shift0, stridePart) : h),
+                "partial pack: bad sizes");
+    ELX_REQUIRE(strideUnion * stridePart == stride, "partial pack: strideUnion * stridePart != stride");
+    const size_t es = DTypeSize(ToDType(dtype));
+    std::vector<kern::Copy2D> d;
+    for (Int k = 0; k < strideUnion; ++k) {
+        const Int sh = Shift(rankPart + k * stridePart, align, stride);
+        ELX_REQUIRE((sh - shift0) % stridePart == 0, "partial pack: shift ", sh, " not on the partial lattice of ", shift0);
+        const Int off = (sh - shift0) / stridePart;
+        const Int len = Length(cols ? h : w, sh, stride);
+        const Int lh = cols ? len : h, lw = cols ? w : len;
+        ELX_REQUIRE(lh * lw <= portionSize, "partial pack: portion ", k, " needs ", lh * lw, " elements");
+        if (lh == 0 || lw == 0) continue;
+        char* m = (char*)M + (cols ? off : off * ldm) * es;
+        char* q = (char*)P + k * portionSize * es;
+        const Int mcs = cols ? strideUnion : 1, mrs = cols ? ldm : strideUnion * ldm;
+        if (pack) d.push_back({lh, lw, m, mcs, mrs, q, 1, lh});
+        else d.push_back({lh, lw, q, 1, lh, m, mcs, mrs});
+    }
+    return d;
+}
+}  // namespace
+
+int elx_pack_strided(int device, int dtype, int64_t height, int64_t width, int64_t colAlign, int64_t colStride,
+                     int64_t rowAlign, int64_t rowStride, const void* A, int64_t lda, void* portions,
+                     int64_t portionSize, void* stream) {
+    return Guard([&] {
+        RunCopies(device, dtype,
+                  StridedPlan(dtype, height, width, colAlign, colStride, rowAlign, rowStride, A, lda, portions,
+                              portionSize, true),
+                  false, 0.0, stream);
+    });
+}
+int elx_unpack_strided(int device, int dtype, int64_t height, int64_t width, int64_t colAlign, int64_t colStride,
+                       int64_t rowAlign, int64_t rowStride, const void* portions, int64_t portionSize, void* B,
+                       int64_t ldb, void* stream) {
+    return Guard([&] {
+        RunCopies(device, dtype,
+                  StridedPlan(dtype, height, width, colAlign, colStride, rowAlign, rowStride, B, ldb, portions,
+                              portionSize, false),
+                  false, 0.0, stream);
+    });
+}
+int elx_pack_partial_strided(int device, int dtype, int cols, int64_t height, int64_t width, int64_t align,
+                             int64_t stride, int64_t strideUnion, int64_t stridePart, int64_t rankPart,
+                             int64_t shiftA, const void* A, int64_t lda, void* portions, int64_t portionSize,
+                             void* stream) {
+    return Guard([&] {
+        RunCopies(device, dtype,
+                  PartialPlan(dtype, cols != 0, height, width, align, stride, strideUnion, stridePart, rankPart,
+                              shiftA, A, lda, portions, portionSize, true),
+                  false, 0.0, stream);
+    });
+}
+int elx_unpack_partial_strided(int device, int dtype, int cols, int64_t height, int64_t width, int64_t align,
+                               int64_t stride, int64_t strideUnion, int64_t stridePart, int64_t rankPart,
+                               int64_t shiftB, const void* portions, int64_t portionSize, void* B, int64_t ldb,
+                               void* stream) {
+    return Guard([&] {
+        RunCopies(device, dtype,
+                  PartialPlan(dtype, cols != 0, height, width, align, stride, strideUnion, stridePart, rankPart,
+                              shiftB, B, ldb, portions, portionSize, false),
+                  false, 0.0, stream);
+    });
+}
+int elx_unpack_axpy_strided(int device, int dtype, int64_t height, int64_t width, double alpha, int64_t colAlign,
+                            int64_t colStride, int64_t rowAlign, int64_t rowStride, const void* portions,
+                            int64_t portionSize, void* B, int64_t ldb, void* stream) {
+    return Guard([&] {  // the fused reduce-scatter epilogue: B(lattice k,l) += alpha * portion (Axpy/util.hpp:23-50)
+        RunCopies(device, dtype,
+                  StridedPlan(dtype, height, width, colAlign, colStride, rowAlign, rowStride, B, ldb, portions,
+                              portionSize, false),
+                  true, alpha, stream);
+    });
+}
 int elx_transpose(int dtype, int64_t m, int64_t n, const void* A, int64_t lda, void* B, int64_t ldb, void* stream) {
     return Guard([&] {  // B (n x m) = A^T
         kern::Copy2D d{n, m, A, lda, 1, B, 1, ldb};
@@ -279,6 +403,39 @@ int elx_comm_reduce_scatter(elx_comm_t c, int dtype, const void* send, void* rec
     });
 }
 int elx_comm_barrier(elx_comm_t c) { return Guard([&] { c->c->Barrier(); }); }
+// the rest of El::mpi's typed collectives (src/core/imports/mpi/*.hpp); counts in
+// elements, device from the communicator's kind, as above
+namespace {
+Device CommDev(elx_comm_t c) { return c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU; }
+hipStream_t CommStream(elx_comm_t c, void* stream) { return CommDev(c) == Device::GPU ? S(stream) : nullptr; }
+}  // namespace
+int elx_comm_split(elx_comm_t c, int color, int key, elx_comm_t* out) {
+    return Guard([&] { *out = new elx_comm_s{c->c->Split(color, key)}; });
+}
+int elx_comm_allreduce(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
+    return Guard([&] { c->c->AllReduce(ToDType(dtype), send, recv, count, CommDev(c), CommStream(c, stream)); });
+}
+int elx_comm_bcast(elx_comm_t c, int dtype, void* buf, int64_t count, int root, void* stream) {
+    return Guard([&] {
+        ELX_REQUIRE(root >= 0 && root < c->c->Size(), "bcast: root ", root, " outside the communicator");
+        c->c->Bcast(ToDType(dtype), buf, count, root, CommDev(c), CommStream(c, stream));
+    });
+}
+int elx_comm_alltoall(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
+    return Guard([&] {  // El::mpi::AllToAll (AllToAll.hpp:11-105): `count` elements to and from every rank
+        const int p = c->c->Size();
+        std::vector<Int> cnt(p, count), dsp(p);
+        for (int q = 0; q < p; ++q) dsp[q] = (Int)q * count;
+        c->c->AllToAllV(ToDType(dtype), send, cnt, dsp, recv, cnt, dsp, CommDev(c), CommStream(c, stream));
+    });
+}
+int elx_comm_sendrecv(elx_comm_t c, int dtype, const void* send, int dest, void* recv, int src, int64_t count,
+                      void* stream) {
+    return Guard([&] {
+        ELX_REQUIRE(dest >= 0 && dest < c->c->Size() && src >= 0 && src < c->c->Size(), "sendrecv: peer outside the communicator");
+        c->c->SendRecv(ToDType(dtype), send, dest, recv, src, count, CommDev(c), CommStream(c, stream));
+    });
+}
 int elx_comm_stats(int64_t* bytes, double* seconds, int64_t* calls) {
     return Guard([&] {
         auto& s = GlobalCommStats();

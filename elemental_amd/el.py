@@ -101,6 +101,38 @@ class Comm:
     def barrier(self):
         call("elx_comm_barrier", self.h)
 
+    # typed collectives on host (numpy) buffers for host comms, device pointers
+    # (ints) for RCCL comms; counts in elements (El::mpi::*, src/core/imports/mpi)
+    def split(self, color: int, key: int) -> "Comm":
+        h = c_void_p()
+        call("elx_comm_split", self.h, color, key, byref(h))
+        return Comm(h, keepalive=self)
+
+    def allgather(self, dtype: int, send, recv, count: int, stream=None):
+        call("elx_comm_allgather", self.h, dtype, _ptr(send), _ptr(recv), count, stream)
+
+    def reduce_scatter(self, dtype: int, send, recv, count: int, stream=None):
+        call("elx_comm_reduce_scatter", self.h, dtype, _ptr(send), _ptr(recv), count, stream)
+
+    def allreduce(self, dtype: int, send, recv, count: int, stream=None):
+        call("elx_comm_allreduce", self.h, dtype, _ptr(send), _ptr(recv), count, stream)
+
+    def bcast(self, dtype: int, buf, count: int, root: int, stream=None):
+        call("elx_comm_bcast", self.h, dtype, _ptr(buf), count, root, stream)
+
+    def alltoall(self, dtype: int, send, recv, count: int, stream=None):
+        call("elx_comm_alltoall", self.h, dtype, _ptr(send), _ptr(recv), count, stream)
+
+    def sendrecv(self, dtype: int, send, dest: int, recv, src: int, count: int, stream=None):
+        call("elx_comm_sendrecv", self.h, dtype, _ptr(send), dest, _ptr(recv), src, count, stream)
+
+
+def _ptr(x):
+    """numpy array -> its data pointer; int / None -> as is (device pointers)."""
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data_as(c_void_p)
+    return x
+
 
 # --------------------------------------------------------------------- grid
 class Grid:

@@ -54,8 +54,7 @@ class GlooBridge:
             elif op == L.COLL_ALLGATHER:
                 s = _arr(send, count, dtype).clone()
                 r = _arr(recv, count * n, dtype)
-                outs = [torch.empty_like(s) for _ in range(n)]
-                dist.all_gather(outs, s, group=pg)
+                outs = self._gather(s, pg, ranks)
                 if count:
                     r.copy_(torch.cat(outs))
             elif op == L.COLL_REDUCE_SCATTER:  # gloo has no reduce_scatter: all-reduce, keep my slice
@@ -73,8 +72,7 @@ class GlooBridge:
                     _arr(recv, count, dtype).copy_(acc.to(s.dtype))
             elif op == L.COLL_ALLTOALL:  # gloo has no all_to_all: gather everything, keep my column
                 s = _arr(send, count * n, dtype).clone()
-                outs = [torch.empty_like(s) for _ in range(n)]
-                dist.all_gather(outs, s, group=pg)
+                outs = self._gather(s, pg, ranks)
                 r = _arr(recv, count * n, dtype)
                 if count:
                     r.copy_(torch.cat([o[me * count:(me + 1) * count] for o in outs]))
@@ -102,6 +100,15 @@ class GlooBridge:
             import sys
             print(f"GlooBridge op {op} failed: {e!r}", file=sys.stderr)
             return 1
+
+    @staticmethod
+    def _gather(s: torch.Tensor, pg, ranks):
+        """all_gather in THIS group's rank order: torch numbers a new_group's
+        members in ascending global rank, a Split orders them by key."""
+        outs = [torch.empty_like(s) for _ in ranks]
+        dist.all_gather(outs, s, group=pg)
+        by_global = dict(zip(sorted(ranks), outs))
+        return [by_global[g] for g in ranks]
 
     def _split(self, ctx, group, color, key, out_group, out_rank, out_size):
         try:

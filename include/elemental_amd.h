@@ -176,6 +176,38 @@ int elx_matrix_copy(int dtype, int device, int64_t m, int64_t n, const void* A, 
 int elx_axpy2d(int dtype, int64_t m, int64_t n, double alpha,
                const void* X, int64_t xcs, int64_t xrs,
                void* Y, int64_t ycs, int64_t yrs, void* stream);
+/* pack / unpack of redistribution portions (include/El/blas_like/level1/Copy/util.hpp),
+ * each ONE batched strided-copy launch over every portion; device = ELX_DEVICE_*.
+ * Portion k + l*colStride holds rows Shift_(k,colAlign,colStride) + i*colStride
+ * and columns Shift_(l,rowAlign,rowStride) + j*rowStride, column-major with ld =
+ * its height; portionSize (elements) must hold the largest portion.
+ *   elx_pack_strided:   StridedPack (util.hpp:667-691); rowStride = 1 is
+ *                       ColStridedPack (:359-378), colStride = 1 RowStridedPack (:148-166)
+ *   elx_unpack_strided: StridedUnpack (:694-718) / ColStridedUnpack / RowStridedUnpack
+ *   elx_pack_partial_strided / elx_unpack_partial_strided: PartialColStrided*
+ *                       (cols = 1, util.hpp:460-552) and PartialRowStrided* (cols = 0,
+ *                       :186-230); stride = strideUnion * stridePart, shiftA/B = the
+ *                       local matrix's own shift on the partial lattice
+ *   elx_unpack_axpy_strided: the fused reduce-scatter epilogue, B += alpha * portion
+ *                       (axpy::util::InterleaveMatrixUpdate, Axpy/util.hpp:23-50) */
+int elx_pack_strided(int device, int dtype, int64_t height, int64_t width,
+                     int64_t colAlign, int64_t colStride, int64_t rowAlign, int64_t rowStride,
+                     const void* A, int64_t lda, void* portions, int64_t portionSize, void* stream);
+int elx_unpack_strided(int device, int dtype, int64_t height, int64_t width,
+                       int64_t colAlign, int64_t colStride, int64_t rowAlign, int64_t rowStride,
+                       const void* portions, int64_t portionSize, void* B, int64_t ldb, void* stream);
+int elx_pack_partial_strided(int device, int dtype, int cols, int64_t height, int64_t width,
+                             int64_t align, int64_t stride, int64_t strideUnion, int64_t stridePart,
+                             int64_t rankPart, int64_t shiftA, const void* A, int64_t lda,
+                             void* portions, int64_t portionSize, void* stream);
+int elx_unpack_partial_strided(int device, int dtype, int cols, int64_t height, int64_t width,
+                               int64_t align, int64_t stride, int64_t strideUnion, int64_t stridePart,
+                               int64_t rankPart, int64_t shiftB, const void* portions,
+                               int64_t portionSize, void* B, int64_t ldb, void* stream);
+int elx_unpack_axpy_strided(int device, int dtype, int64_t height, int64_t width, double alpha,
+                            int64_t colAlign, int64_t colStride, int64_t rowAlign, int64_t rowStride,
+                            const void* portions, int64_t portionSize, void* B, int64_t ldb,
+                            void* stream);
 int elx_copy2d(int dtype, int64_t m, int64_t n,
                const void* A, int64_t acs, int64_t ars,
                void* B, int64_t bcs, int64_t brs, void* stream);
@@ -242,6 +274,19 @@ int elx_comm_allgather(elx_comm_t comm, int dtype, const void* send, void* recv,
 int elx_comm_reduce_scatter(elx_comm_t comm, int dtype, const void* send, void* recv,
                             int64_t count, void* stream);
 int elx_comm_barrier(elx_comm_t comm);
+/* the rest of El::mpi's typed collectives (src/core/imports/mpi/{AllReduce,
+ * Broadcast.hpp:11-107, AllToAll.hpp:11-105, SendRecv.hpp:9-60}, mpi.cpp:438-441
+ * for Split): counts in elements; RCCL comms take device buffers on `stream`,
+ * host comms host buffers */
+int elx_comm_split(elx_comm_t comm, int color, int key, elx_comm_t* out);
+int elx_comm_allreduce(elx_comm_t comm, int dtype, const void* send, void* recv,
+                       int64_t count, void* stream);
+int elx_comm_bcast(elx_comm_t comm, int dtype, void* buf, int64_t count, int root,
+                   void* stream);
+int elx_comm_alltoall(elx_comm_t comm, int dtype, const void* send, void* recv,
+                      int64_t count, void* stream);
+int elx_comm_sendrecv(elx_comm_t comm, int dtype, const void* send, int dest,
+                      void* recv, int src, int64_t count, void* stream);
 /* cumulative traffic counters of the collectives issued by this process */
 int elx_comm_stats(int64_t* bytes_moved, double* seconds, int64_t* calls);
 int elx_comm_stats_reset(void);

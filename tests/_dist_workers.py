@@ -736,3 +736,67 @@ def half_sum_worker(rank: int, world: int, port: int, seed: int):
     except Exception:
         traceback.print_exc()
         raise
+
+
+def raw_coll_worker(rank: int, world: int, port: int):
+    """The raw El::mpi collectives of the C-ABI (elx_comm_*) on the world and on
+    a Split of it: AllGather, ReduceScatter (SUM), AllReduce (SUM), Bcast,
+    AllToAll, SendRecv (src/core/imports/mpi/*.hpp), exact integer-valued f64."""
+    el, comm = init(rank, world, port)
+    rccl = os.environ.get("ELX_TEST_BACKEND") == "rccl"
+    if rccl:  # RCCL comms take device buffers
+        import torch
+        from elemental_amd import _lib as L
+
+        class Dev:
+            def __init__(self, a):
+                self.t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+                torch.cuda.synchronize()
+
+            def np(self):
+                L.call("elx_device_synchronize")
+                return self.t.cpu().numpy()
+        buf = lambda a: Dev(a)
+        ptr = lambda b: b.t.data_ptr()
+        get = lambda b: b.np()
+    else:
+        buf = lambda a: np.array(a, dtype=np.float64)
+        ptr = lambda b: b
+        get = lambda b: b
+    try:
+        def check(c, tag):
+            p, r = c.size, c.rank
+            n = 5
+            mine_h = np.arange(n, dtype=np.float64) + 100 * r
+            mine, out = buf(mine_h), buf(np.zeros(n * p))
+            c.allgather(el.F64, ptr(mine), ptr(out), n)
+            assert np.array_equal(get(out), np.concatenate([np.arange(n) + 100 * q for q in range(p)])), tag
+            send = buf(np.concatenate([np.arange(n) + 10 * q + r for q in range(p)]).astype(np.float64))
+            rs = buf(np.zeros(n))
+            c.reduce_scatter(el.F64, ptr(send), ptr(rs), n)
+            assert np.array_equal(get(rs), p * (np.arange(n) + 10 * r) + sum(range(p))), tag
+            ar = buf(np.zeros(n))
+            c.allreduce(el.F64, ptr(mine), ptr(ar), n)
+            assert np.array_equal(get(ar), p * np.arange(n) + 100 * sum(range(p))), tag
+            root = p - 1
+            b = buf(mine_h.copy())
+            c.bcast(el.F64, ptr(b), n, root)
+            assert np.array_equal(get(b), np.arange(n) + 100 * root), tag
+            a2a_send = buf(np.concatenate([np.full(n, 1000 * r + q, dtype=np.float64) for q in range(p)]))
+            a2a = buf(np.zeros(n * p))
+            c.alltoall(el.F64, ptr(a2a_send), ptr(a2a), n)
+            assert np.array_equal(get(a2a), np.concatenate([np.full(n, 1000 * q + r) for q in range(p)])), tag
+            ring = buf(np.zeros(n))
+            c.sendrecv(el.F64, ptr(mine), (r + 1) % p, ptr(ring), (r - 1) % p, n)
+            assert np.array_equal(get(ring), np.arange(n) + 100 * ((r - 1) % p)), tag
+
+        check(comm, "world")
+        sub = comm.split(rank % 2, -rank)  # key reverses the order inside each half
+        members = [q for q in range(world) if q % 2 == rank % 2]
+        assert sub.size == len(members)
+        assert sub.rank == sorted(members, reverse=True).index(rank)
+        check(sub, "split")
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise

@@ -92,6 +92,13 @@ def test_host_backend_16bit_sums():
     _spawn(W.half_sum_worker, 4, 3)
 
 
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_raw_collectives(world):
+    """elx_comm_{allgather,reduce_scatter,allreduce,bcast,alltoall,sendrecv,split}
+    on the host backend, on the world and on a split with reversed keys."""
+    _spawn(W.raw_coll_worker, world)
+
+
 @pytest.mark.parametrize("world,height,cols", [(1, 1, 0), (2, 1, 0), (4, 2, 0), (1, 1, 3), (4, 2, 2), (2, 2, 5)])
 def test_syrk_herk(world, height, cols, monkeypatch):
     """El::Syrk / El::Herk LN/LT/UN/UT on 1x1, 1x2, 2x1 and 2x2 grids (Syrk/*.hpp);

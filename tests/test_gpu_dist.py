@@ -218,6 +218,8 @@ def test_gpu_rccl_single_rank_redistribution_and_summa():
     # multistream teams over RCCL: each team's grid is a split duplicate of the world
     _rccl_spawn(W.gemm_worker, 1, 1, el.GPU, el.F64, [(45, 37, 61)],
                 [el.GEMM_SUMMA_C_MS, el.GEMM_SUMMA_A_MS, el.GEMM_DEFAULT], 16, 7, 16, 3)
+    # the raw El::mpi collectives of the C-ABI (incl. Split, Bcast, AllToAll, SendRecv) on device buffers
+    _rccl_spawn(W.raw_coll_worker, 1)
 
 
 @pytest.mark.skipif(el.device_count() < 2, reason="needs >= 2 GPUs (one RCCL rank per GPU)")
@@ -229,6 +231,7 @@ def test_gpu_rccl_multi_gpu(world, height):
     _rccl_spawn(W.gemm_worker, world, min(height, world), el.GPU, el.F64, [(45, 37, 61)], algs, 16, 6)
     _rccl_spawn(W.gemm_worker, world, min(height, world), el.GPU, el.F64, [(45, 37, 130)],
                 [el.GEMM_SUMMA_C, el.GEMM_SUMMA_C_MS, el.GEMM_SUMMA_A_MS], 16, 8, 16, 2)
+    _rccl_spawn(W.raw_coll_worker, world)
 
 
 def test_gpu_attach_torch_storage():

@@ -321,3 +321,37 @@ def test_copy2d_convert(s, t):
     L.call("elx_copy2d_convert", s, t, mh, nh, dX.data_ptr(), 2, 2 * m, dS.data_ptr(), 1, mh, None)
     sync()
     assert same(host(dS, (mh, nh), ht), want[::2, ::2])
+
+
+@pytest.mark.parametrize("h,w,ca,cs,ra,rs", [(1000, 37, 3, 4, 1, 2), (129, 65, 0, 2, 0, 4), (7, 300, 1, 8, 0, 1)])
+def test_gpu_pack_unpack_strided(h, w, ca, cs, ra, rs):
+    """elx_pack_strided / elx_unpack_strided / elx_unpack_axpy_strided on device
+    buffers (one batched launch each) against the numpy restatement of
+    StridedPack / StridedUnpack (Copy/util.hpp:667-718)."""
+    import torch
+    import test_pack_cpu as P
+    ld = h + 5
+    A = P.padded(h, w, ld, 4)
+    ps = -(-h // cs) * -(-w // rs) + 3
+    want = np.full(cs * rs * ps, np.nan)
+    for l in range(rs):
+        rsh = P.shift(l, ra, rs)
+        for k in range(cs):
+            csh = P.shift(k, ca, cs)
+            sub = A[csh:h:cs, rsh:w:rs]
+            q = (k + l * cs) * ps
+            want[q:q + sub.size] = sub.ravel(order="F")
+    Ad = torch.from_numpy(np.ascontiguousarray(A.T)).cuda()  # column-major ld x w
+    Pd = torch.full((cs * rs * ps,), float("nan"), dtype=torch.float64, device="cuda")
+    Bd = torch.full_like(Ad, -7.0)
+    torch.cuda.synchronize()
+    L.call("elx_pack_strided", 1, el.F64, h, w, ca, cs, ra, rs, Ad.data_ptr(), ld, Pd.data_ptr(), ps, None)
+    L.call("elx_unpack_strided", 1, el.F64, h, w, ca, cs, ra, rs, Pd.data_ptr(), ps, Bd.data_ptr(), ld, None)
+    L.call("elx_device_synchronize")
+    assert np.array_equal(Pd.cpu().numpy(), want, equal_nan=True)
+    B = Bd.cpu().numpy().T
+    assert np.array_equal(B[:h, :w], A[:h, :w]) and np.all(B[h:, :] == -7.0)
+    L.call("elx_unpack_axpy_strided", 1, el.F64, h, w, -2.0, ca, cs, ra, rs, Pd.data_ptr(), ps, Bd.data_ptr(), ld,
+           None)
+    L.call("elx_device_synchronize")
+    assert np.array_equal(Bd.cpu().numpy().T[:h, :w], -A[:h, :w])
