@@ -280,7 +280,7 @@ def test_pool_alloc_free():
             round_trip(s2, s1)
             round_trip(s1, s2)
         r2, _ = el.pool_stats()
-        assert r2 == r1, (r1, r2)
+        assert r2 <= r1, (r1, r2)  # nothing new reserved (the driver may release idle pages)
         L.call("elx_pool_trim", 0)
         r3, _ = el.pool_stats()
         assert r3 <= r2
