@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <utility>
 #include "kernels.hpp"
 #include "lds_dma.hpp"
 #include "elem.hpp"
@@ -178,8 +179,8 @@ __device__ __forceinline__ void step(const Frame& f, i64 knext, bool more, lds_c
     }
 }
 
-template <bool BF16>
-__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][4], i64 m0, i64 n0, int wr, int wc,
+template <bool BF16, int NI = 4>
+__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][NI], i64 m0, i64 n0, int wr, int wc,
                                          int l);
 
 // KCA: op(A) k-contiguous (TA); KCB: op(B) k-contiguous (!TB).
@@ -500,45 +501,50 @@ __global__ __launch_bounds__(NT, 1) void gemm_h8b_kernel(H2Params p) {
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
-// C = alpha acc + beta C.  C/D map of 16x16x32: col = lane&15, rows 4*(lane>>4) + r
-// (r = 0..3), i.e. four consecutive rows of one column = one 8-B access per tile.
+// One 16 x 16 accumulator tile: rows i..i+15 (4 per lane), column j.
 template <bool BF16>
-__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][4], i64 m0, i64 n0, int wr, int wc,
-                                         int l) {
+__device__ __forceinline__ void epi_one(const H2Params& p, const f32x4 v4, i64 i, i64 j) {
     using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
-    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 64 + (l & 15);
+    if (j >= p.n || i >= p.m) return;
+    uint16_t* o = p.C + i + j * p.ldc;
+    if (p.vec_c && i + 3 < p.m) {
+        uint2 cv = make_uint2(0, 0);
+        if (p.beta != 0.f) cv = *reinterpret_cast<const uint2*>(o);
+        const uint16_t in[4] = {(uint16_t)(cv.x & 0xffff), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xffff),
+                                (uint16_t)(cv.y >> 16)};
+        uint16_t r16[4];
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
+        for (int r = 0; r < 4; ++r) {
+            float v = p.alpha * v4[r];
+            if (p.beta != 0.f) v += p.beta * E::load(in[r]);
+            r16[r] = E::store(v);
+        }
+        *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16),
+                                                  (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+    } else {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            const i64 i = rb + mi * 16, j = cb + ni * 16;
-            if (j >= p.n || i >= p.m) continue;
-            uint16_t* o = p.C + i + j * p.ldc;
-            if (p.vec_c && i + 3 < p.m) {
-                uint2 cv = make_uint2(0, 0);
-                if (p.beta != 0.f) cv = *reinterpret_cast<const uint2*>(o);
-                const uint16_t in[4] = {(uint16_t)(cv.x & 0xffff), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xffff),
-                                        (uint16_t)(cv.y >> 16)};
-                uint16_t r16[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = p.alpha * acc[mi][ni][r];
-                    if (p.beta != 0.f) v += p.beta * E::load(in[r]);
-                    r16[r] = E::store(v);
-                }
-                *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16),
-                                                          (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (i + r >= p.m) break;
-                    float v = p.alpha * acc[mi][ni][r];
-                    if (p.beta != 0.f) v += p.beta * E::load(o[r]);
-                    o[r] = E::store(v);
-                }
-            }
+        for (int r = 0; r < 4; ++r) {
+            if (i + r >= p.m) break;
+            float v = p.alpha * v4[r];
+            if (p.beta != 0.f) v += p.beta * E::load(o[r]);
+            o[r] = E::store(v);
         }
     }
+}
+
+// every tile with compile-time indices (a fold, not a loop: a loop the unroller
+// declines would index the accumulators dynamically and push them to scratch)
+template <bool BF16, int NI, int... Q>
+__device__ __forceinline__ void epilogue_seq(const H2Params& p, const f32x4 (&acc)[8][NI], i64 rb, i64 cb,
+                                             std::integer_sequence<int, Q...>) {
+    (epi_one<BF16>(p, acc[Q / NI][Q % NI], rb + (Q / NI) * 16, cb + (Q % NI) * 16), ...);
+}
+
+template <bool BF16, int NI>
+__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][NI], i64 m0, i64 n0, int wr, int wc,
+                                         int l) {
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * (16 * NI) + (l & 15);
+    epilogue_seq<BF16, NI>(p, acc, rb, cb, std::make_integer_sequence<int, 8 * NI>{});
 }
 
 template <typename K>
