@@ -113,6 +113,7 @@ _SIGS = {
     "elx_dm_buffer": (_i, [_vp, POINTER(c_void_p)]),
     "elx_dm_set_local": (_i, [_vp, _vp, _i64]),
     "elx_dm_get_local": (_i, [_vp, _vp, _i64]),
+    "elx_dm_frobenius_norm": (_i, [_vp, POINTER(c_double)]),
     "elx_dm_view": (_i, [POINTER(c_void_p), _vp, _i64, _i64, _i64, _i64]),
     "elx_dm_attach": (_i, [_vp, _i64, _i64, _i, _i, _vp, _i64, _i]),
     "elx_dm_copy": (_i, [_vp, _vp]),

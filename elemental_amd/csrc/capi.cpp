@@ -489,6 +489,7 @@ int elx_dm_info(elx_dm_t A, int64_t* info) {
 int elx_dm_buffer(elx_dm_t A, void** ptr) { return Guard([&] { *ptr = M(A).Buffer(); }); }
 int elx_dm_set_local(elx_dm_t A, const void* host, int64_t ld) { return Guard([&] { M(A).SetLocal(host, ld); }); }
 int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld) { return Guard([&] { M(A).GetLocal(host, ld); }); }
+int elx_dm_frobenius_norm(elx_dm_t A, double* out) { return Guard([&] { *out = FrobeniusNorm(M(A)); }); }
 int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1) {
     return Guard([&] { *V = new elx_dm_s{DistMatrix::View(M(A), i0, i1, j0, j1)}; });
 }

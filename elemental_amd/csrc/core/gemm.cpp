@@ -30,6 +30,7 @@
 #include "exec.hpp"
 #include <algorithm>
 #include <functional>
+#include "../runtime/trace.hpp"
 #include <initializer_list>
 #include <vector>
 
@@ -401,6 +402,7 @@ void TrrkLocal(bool lower, bool ta, bool tb, Int k, double alpha, const void* a,
 // upper (ELX_UPPER) triangle is updated, through TrrkLocal.
 void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
             DistMatrix& CPre, int uplo = -1) {
+    ELX_TRACE(uplo >= 0 ? "El::Trrk SUMMA_C" : "El::Gemm SUMMA_C");
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
@@ -449,6 +451,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
     Buffer trrk_tmp;
 
     auto issue = [&](int p) {
+        ELX_TRACE("SUMMA_C panel gather");
         Slot& s = slot[p & 1];
         const Int k0 = p * kc, k1 = std::min(K, k0 + kc);
         if (gpu && s.pending) ELX_CHECK_HIP(hipStreamWaitEvent(ms, s.done, 0));
@@ -470,6 +473,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         if (gpu) ELX_CHECK_HIP(hipEventRecord(s.ready, ms));
     };
     auto compute = [&](int p) {
+        ELX_TRACE("SUMMA_C panel update");
         Slot& s = slot[p & 1];
         const DistMatrix& a = *s.ua;
         const DistMatrix& b = *s.ub;
@@ -526,6 +530,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // ---------------------------------------------------------------------------
 void SummaCMultistream(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, double beta,
                        DistMatrix& CPre) {
+    ELX_TRACE("El::Gemm SUMMA_C_MS");
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
@@ -610,6 +615,7 @@ void SummaCMultistream(int oA, int oB, double alpha, const DistMatrix& APre, con
 // communicators and temporaries; the C panels are disjoint, so no C copies.
 void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
             bool ms = false) {
+    ELX_TRACE("El::Gemm SUMMA_A");
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
@@ -655,6 +661,7 @@ void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // ---------------------------------------------------------------------------
 void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
             bool ms = false) {
+    ELX_TRACE("El::Gemm SUMMA_B");
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
@@ -701,6 +708,7 @@ void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 // ---------------------------------------------------------------------------
 void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre,
               Int bs) {
+    ELX_TRACE("El::Gemm SUMMA_DOT");
     const Int m = CPre.Height(), n = CPre.Width();
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
     // k must be distributed VC on both: op(A) = A ([*,VC]) or A^T ([VC,*])
@@ -736,6 +744,7 @@ void SummaDot(int oA, int oB, double alpha, const DistMatrix& APre, const DistMa
 // one local MFMA update with beta = 1.
 // ---------------------------------------------------------------------------
 void Cannon(double alpha, const DistMatrix& APre, const DistMatrix& BPre, DistMatrix& CPre) {
+    ELX_TRACE("El::Gemm CANNON");
     const Grid& g = CPre.G();
     if (g.Height() != g.Width()) throw LogicError("Process grid must be square for Cannon's");
     MultiSync sync(CPre.Stream(), {APre.Stream(), BPre.Stream()});
@@ -867,6 +876,7 @@ void ProfileStats(double& gemm_ms, int64_t& launches, double& flops, double& com
 }
 
 void LocalGemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C) {
+    ELX_TRACE("El::LocalGemm");
     ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "LocalGemm: mixed types");
     ELX_REQUIRE(A.Dev() == B.Dev() && A.Dev() == C.Dev(), "LocalGemm: mixed devices");
     // the reference's conformance checks (src/blas_like/level3/Gemm.cpp:326-423)
@@ -924,6 +934,7 @@ void ScaleTrapezoid(double alpha, int uplo, DistMatrix& A, Int offset) {
 // variant when width > 10 height (LN.hpp:156); here the panel pipeline serves
 // every shape (same sums, summation order within the normwise tolerance).
 void Syrk(int uplo, int orient, double alpha, const DistMatrix& A, double beta, DistMatrix& C) {
+    ELX_TRACE("El::Syrk");
     ELX_REQUIRE(uplo == ELX_LOWER || uplo == ELX_UPPER, "Syrk: bad UpperOrLower ", uplo);
     ELX_REQUIRE(orient >= ELX_NORMAL && orient <= ELX_ADJOINT, "Syrk: bad orientation");
     ELX_REQUIRE(&A.G() == &C.G(), "Syrk: matrices on different grids");
@@ -989,6 +1000,7 @@ bool TrsmFlat() {
 }
 
 void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatrix& XPre) {
+    ELX_TRACE("El::Trsm");
     MultiSync sync(XPre.Stream(), {APre.Stream()});
     auto Ap = ReadProxy(APre, XPre, Dist::MC, Dist::MR);
     const DistMatrix& A = *Ap;
@@ -1161,6 +1173,7 @@ void Symm(int side, int uplo, double alpha, const DistMatrix& A, const DistMatri
 
 void Gemm(int oA, int oB, double alpha, const DistMatrix& A, const DistMatrix& B, double beta, DistMatrix& C,
           int alg) {
+    ELX_TRACE("El::Gemm");
     ELX_REQUIRE(oA >= ELX_NORMAL && oA <= ELX_ADJOINT && oB >= ELX_NORMAL && oB <= ELX_ADJOINT, "bad orientation");
     ELX_REQUIRE(&A.G() == &B.G() && &A.G() == &C.G(), "Gemm: matrices on different grids");
     ELX_REQUIRE(A.Type() == B.Type() && A.Type() == C.Type(), "Gemm: mixed types");

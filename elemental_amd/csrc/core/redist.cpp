@@ -20,8 +20,10 @@
 // result is bit-exact by construction (pure data movement).
 #include "redist.hpp"
 #include "exec.hpp"
+#include "../runtime/trace.hpp"
 #include <cstring>
 #include <numeric>
+#include <cmath>
 #include <vector>
 
 namespace elx {
@@ -304,6 +306,7 @@ void CopyConvert(const DistMatrix& A, DistMatrix& B) {
 }
 
 void Copy(const DistMatrix& A, DistMatrix& B) {
+    ELX_TRACE("El::Copy (redistribution)");
     if (A.Type() != B.Type()) { CopyConvert(A, B); return; }
     CheckCompatible(A, B);
     if (A.Dev() != B.Dev()) {
@@ -555,6 +558,25 @@ void Fill(DistMatrix& A, double v) {
 // entry of A exactly zero?  The local diagonal entries form one arithmetic
 // progression (global index step lcm(colStride, rowStride)), gathered by one
 // strided copy; the per-rank answers are summed over the grid.
+double FrobeniusNorm(const DistMatrix& A) {
+    double local = 0.0;
+    const Int lh = A.LocalHeight(), lw = A.LocalWidth();
+    if (A.Participating() && lh > 0 && lw > 0) {
+        const size_t es = A.ElemSize();
+        std::vector<unsigned char> host((size_t)lh * lw * es);
+        A.GetLocal(host.data(), lh);
+        for (size_t q = 0; q < (size_t)lh * lw; ++q) {
+            const double v = exec::LoadScalar(A.Type(), host.data() + q * es);
+            local += v * v;
+        }
+        int copies = 0;  // ranks holding this same local block (replicated distributions)
+        for (int q = 0; q < A.G().Size(); ++q)
+            if (A.ColRankOf(q) == A.ColRank() && A.RowRankOf(q) == A.RowRank()) ++copies;
+        local /= copies;
+    }
+    return std::sqrt(GridAllReduceSum(A.G(), local));
+}
+
 bool DiagonalHasZero(const DistMatrix& A) {
     const Int n = std::min(A.Height(), A.Width());
     double zeros = 0;

@@ -34,6 +34,9 @@ void Update(DistMatrix& A, Int i, Int j, double v);
 void Fill(DistMatrix& A, double v);
 // collective: is any diagonal entry exactly zero?  (Trsm's checkIfSingular)
 bool DiagonalHasZero(const DistMatrix& A);
+// El::FrobeniusNorm (src/lapack_like/norm/Frobenius.cpp): collective over the grid,
+// each entry counted once however many ranks hold a copy of it
+double FrobeniusNorm(const DistMatrix& A);
 // grid-wide scalar sum / broadcast from VC rank `rootVC`
 double GridAllReduceSum(const Grid& g, double v);
 double GridBcast(const Grid& g, double v, int rootVC);

@@ -625,6 +625,12 @@ template <typename T> void EntrywiseMap(const AbstractDistMatrix<T>& A, Abstract
 template <typename T, typename S> void AxpyContract(S alpha, const AbstractDistMatrix<T>& A, AbstractDistMatrix<T>& B) {
     detail::Check(elx_dm_axpy_contract(static_cast<double>(alpha), A.h(), B.h()));
 }
+// El::FrobeniusNorm on DistMatrices (collective; Base<T> is T for the real types)
+template <typename T> double FrobeniusNorm(const AbstractDistMatrix<T>& A) {
+    double v = 0.0;
+    detail::Check(elx_dm_frobenius_norm(A.h(), &v));
+    return v;
+}
 // grid-independent synthetic fill (stands in for Uniform(A, m, n, center, radius) in benchmarks)
 // El::InitializeRandom (random.cpp:24-35); Initialize() seeds deterministically
 inline void InitializeRandom(bool deterministic = true, int worldRank = 0) {
@@ -632,10 +638,10 @@ inline void InitializeRandom(bool deterministic = true, int worldRank = 0) {
 }
 // El::Uniform / MakeUniform (Uniform.cpp:18-66): the reference's draws bit for bit
 template <typename T> void MakeUniform(AbstractDistMatrix<T>& A, T center = T(0), double radius = 1.0) {
-    detail::Check(elx_dm_make_uniform(A.h(), static_cast<double>(center), radius));
+    detail::Check(elx_dm_make_uniform(A.h(), detail::ToDouble(center), radius));
 }
 template <typename T> void Uniform(AbstractDistMatrix<T>& A, Int m, Int n, T center = T(0), double radius = 1.0) {
-    detail::Check(elx_dm_uniform(A.h(), m, n, static_cast<double>(center), radius));
+    detail::Check(elx_dm_uniform(A.h(), m, n, detail::ToDouble(center), radius));
 }
 template <typename T> void HashFill(AbstractDistMatrix<T>& A, std::uint64_t seed, double center, double radius) {
     detail::Check(elx_dm_fill_hash(A.h(), seed, center, radius));

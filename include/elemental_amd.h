@@ -314,6 +314,8 @@ int elx_dm_buffer(elx_dm_t A, void** ptr);
 /* host <-> local buffer (column-major, leading dim ld) */
 int elx_dm_set_local(elx_dm_t A, const void* host, int64_t ld);
 int elx_dm_get_local(elx_dm_t A, void* host, int64_t ld);
+/* El::FrobeniusNorm (collective over the grid; each entry counted once) */
+int elx_dm_frobenius_norm(elx_dm_t A, double* out);
 /* V := A(i0:i1, j0:j1) (a view, El::View / A(IR,IR)) */
 int elx_dm_view(elx_dm_t* V, elx_dm_t A, int64_t i0, int64_t i1, int64_t j0, int64_t j1);
 /* A views caller storage as its local block: ElementalMatrix::Attach

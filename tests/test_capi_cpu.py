@@ -163,3 +163,27 @@ def test_functor_header_compiles_for_gfx950(tmp_path):
     subprocess.check_call([hipcc, "-std=c++17", "-O1", "--offload-arch=gfx950", "-c", "-I", os.path.join(ROOT, "include"),
                            os.path.join(ROOT, "tests", "cpp", "test_entrywise_functor.hip"), "-o",
                            str(tmp_path / "t.o")])
+
+
+def test_gemm_suite_driver_cpu(tmp_path):
+    """tests/cpp/gemm_suite.cpp (built by build()): the reference suite's
+    experiment-file format (Gemm_Suite.cpp:274-276,494-540) on Device::CPU
+    matrices, warm-up associativity residuals enforced (--check), the results
+    file in the suite's format (:617-662)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "gemm_suite")
+    if not os.path.exists(exe):
+        pytest.skip("gemm_suite not built (run __graft_entry__.build())")
+    exp = tmp_path / "exp.txt"
+    exp.write_text("# comment\nCPU:Double:N:N:SUMMA_C:37:29:41:8\nCPU:Double:T:N:SUMMA_A:20:25:33:4\n"
+                   "CPU:Float:N:T:SUMMA_B:18:40:22:8\nCPU:Double:T:T:SUMMA_DOT:12:13:300:16\n"
+                   "CPU:Double:N:N:CANNON:24:24:24:8\nnot an experiment\n")
+    res = tmp_path / "res.txt"
+    r = subprocess.run([exe, "--f", str(exp), "--o", str(res), "--warmup", "2", "--runs", "3", "--check"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("|| E ||_F / || Y ||_F") == 10
+    lines = res.read_text().splitlines()
+    assert [ln.split(":")[:9] for ln in lines][0] == ["CPU", "double", "Normal", "Normal", "SUMMA_C", "37", "29",
+                                                      "41", "8"]
+    assert len(lines) == 5 and all(len(ln.split(":")) == 12 for ln in lines)
+    assert lines[2].startswith("CPU:float:Normal:Transpose:SUMMA_B:")

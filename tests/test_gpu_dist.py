@@ -371,3 +371,27 @@ def test_gpu_trsm_large(dtype):
 def test_gpu_symm_distributed(world, height):
     """El::Symm / El::Hemm on the GPU (trapezoid copy + SUMMA), host-staged ranks."""
     _spawn(W.symm_worker, world, height, el.GPU, el.F64, 45, 29, 61)
+
+
+def test_gpu_gemm_suite_driver(tmp_path):
+    """The reference suite's experiment files run unchanged through the drop-in
+    header on Device::GPU (tests/cpp/gemm_suite.cpp): every algorithm id,
+    double / float / half / bfloat16, warm-up associativity residuals enforced
+    (--check), one results line per experiment in the suite's format."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "_build", "gemm_suite")
+    assert os.path.exists(exe), f"{exe} missing: run __graft_entry__.build()"
+    algs = ["DEFAULT", "SUMMA_A", "SUMMA_B", "SUMMA_C", "SUMMA_DOT", "SUMMA_A_MS", "SUMMA_C_MS", "CANNON"]
+    lines = [f"GPU:Double:N:N:{a}:300:260:520:64" for a in algs]
+    lines += ["GPU:Double:T:N:SUMMA_C:257:129:700:128", "GPU:Float:N:T:SUMMA_C:512:384:640:128",
+              "GPU:Half:N:N:SUMMA_C:512:512:1024:128", "GPU:Bfloat:T:N:SUMMA_C:512:256:512:128",
+              "GPU:Double:T:T:SUMMA_DOT:64:64:20000:128"]
+    exp = tmp_path / "exp.txt"
+    exp.write_text("\n".join(lines) + "\n")
+    res = tmp_path / "res.txt"
+    r = subprocess.run([exe, "--f", str(exp), "--o", str(res), "--warmup", "2", "--runs", "3", "--check"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    out = res.read_text().splitlines()
+    assert len(out) == len(lines) and all(ln.startswith("GPU:") and len(ln.split(":")) == 12 for ln in out)
