@@ -11,13 +11,18 @@
 // runs, each preceded by untimed ones.  Types: D double, F float, H half
 // (gpu_half_type), B bfloat16 (new).  One process, Grid 1x1.
 //
+// Inputs: --fill mt19937 draws A, B, COrig exactly as the reference does
+// (El::Uniform: one host std::mt19937 stream, then a host-to-device copy: ~10 s
+// per 32768^2 matrix); the default --fill hash draws the same distribution from
+// the grid-independent counter hash on the device (El::HashFill), seeds 1, 2, 3.
+//
 // Timing: the device is synchronized around each timed Gemm and the host clock
 // read (the suite reads a hipEvent pair on C's stream; both bracket exactly the
 // one call).  --check makes a warm-up residual above the type's bound fatal
 // (the suite only prints it).
 //
 //   gemm_suite --f experiments.txt --o results.txt [--warmup 5] [--runs 10]
-//              [--skips 2] [--check]
+//              [--skips 2] [--check] [--fill hash|mt19937]
 #include <El.hpp>
 
 #include <chrono>
@@ -45,6 +50,7 @@ struct Options {
     std::string in, out;
     int warmup = 5, runs = 10, skips = 2;
     bool check = false;
+    bool mt19937 = false;
 };
 
 const char* kAlgNames[] = {"DEFAULT", "SUMMA_A_MS", "SUMMA_A", "SUMMA_B_MS", "SUMMA_B",
@@ -153,9 +159,18 @@ std::vector<double> Run(const Experiment& e, const Options& o, const El::Grid& g
     const El::Int br = e.ob == El::NORMAL ? e.k : e.n, bc = e.ob == El::NORMAL ? e.n : e.k;
     DM<T, D> A(g), B(g), COrig(g), C(g);
     const T c0 = El::detail::FromDouble<T>(-0.1);
-    El::Uniform(A, ar, ac, c0, 0.1);
-    El::Uniform(B, br, bc, c0, 0.1);
-    El::Uniform(COrig, e.m, e.n, c0, 0.1);
+    if (o.mt19937) {
+        El::Uniform(A, ar, ac, c0, 0.1);
+        El::Uniform(B, br, bc, c0, 0.1);
+        El::Uniform(COrig, e.m, e.n, c0, 0.1);
+    } else {
+        A.Resize(ar, ac);
+        B.Resize(br, bc);
+        COrig.Resize(e.m, e.n);
+        El::HashFill(A, 1, -0.1, 0.1);
+        El::HashFill(B, 2, -0.1, 0.1);
+        El::HashFill(COrig, 3, -0.1, 0.1);
+    }
     std::printf("  Correctness tests:\n");
     for (int i = 0; i < o.warmup; ++i) {
         C = COrig;
@@ -215,11 +230,20 @@ int main(int argc, char** argv) {
         else if (a == "--skips") o.skips = std::atoi(next().c_str());
         else if (a == "--gridHeight") next();  // one process: the grid is 1x1
         else if (a == "--check") o.check = true;
+        else if (a == "--fill") {
+            const std::string f = next();
+            if (f != "hash" && f != "mt19937") {
+                std::fprintf(stderr, "--fill hash|mt19937\n");
+                return 2;
+            }
+            o.mt19937 = f == "mt19937";
+        }
         else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
         }
     }
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // progress lines as they happen
     El::Initialize(argc, argv);
     std::vector<Experiment> suite;
     {
