@@ -44,7 +44,7 @@ PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3, "bf16": 2500.0, "f16": 2500.0}
 HBM_PEAK_GBS = 8000.0
 METRIC = "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak"
 KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_f32g_kernel (LDS-DMA)",
-          "bf16": "gemm_h8p_kernel<bf16>", "f16": "gemm_h8p_kernel<f16>"}
+          "bf16": "gemm_h8b_kernel<bf16>", "f16": "gemm_h8b_kernel<f16>"}
 
 
 def cpu_baseline(seconds_target: float = 10.0) -> dict:
@@ -197,16 +197,25 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
-    L.call("elx_set_device", local)
-    torch.cuda.set_device(local)
+    # ELX_BENCH_COMM=host: rehearsal of the N>1 line on a one-GPU box — every
+    # rank on device 0, panels host-staged over gloo instead of RCCL (RCCL refuses
+    # two ranks on one GPU); never the driver's configuration
+    rehearse = world > 1 and os.environ.get("ELX_BENCH_COMM") == "host"
+    dev = 0 if rehearse else local
+    L.call("elx_set_device", dev)
+    torch.cuda.set_device(dev)
 
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane only (uid, barrier, max); data goes over RCCL
-        obj = [el.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = el.Comm.rccl(rank, world, obj[0])
+        if rehearse:
+            from elemental_amd.torch_bridge import GlooBridge
+            comm = el.Comm.host(GlooBridge())
+        else:
+            obj = [el.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = el.Comm.rccl(rank, world, obj[0])
     else:
         comm = el.Comm.self_comm()
     grid = el.Grid(comm, 0)
@@ -306,6 +315,7 @@ def main():
             "blocksize": args.nb,
             "compute_panel": args.kc or "auto",
             "parallelism": f"grid{gshape}",
+            **({"comm": "host-staged gloo, all ranks on device 0 (rehearsal)"} if rehearse else {}),
         },
         "pct_of_mfma_peak": round(100.0 * value / (peak * world), 2),
         "roofline": {

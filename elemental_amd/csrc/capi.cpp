@@ -215,6 +215,7 @@ int elx_copy2d_convert(int src_dtype, int dst_dtype, int64_t m, int64_t n, const
 // issues one InterleaveMatrix per portion).  Portion k of a colStride-way split
 // holds the rows colShift(k) = Shift_(k, colAlign, colStride), colShift+colStride, ...
 // (indexing/impl.hpp:33-36,244-245), stored column-major with ld = its height.
+}  // extern "C"
 namespace {
 Device PackDev(int device) {
     ELX_REQUIRE(device == ELX_DEVICE_CPU || device == ELX_DEVICE_GPU, "pack: bad device ", device);
@@ -281,6 +282,7 @@ std::vector<kern::Copy2D> PartialPlan(int dtype, bool cols, Int h, Int w, Int al
     return d;
 }
 }  // namespace
+extern "C" {
 
 int elx_pack_strided(int device, int dtype, int64_t height, int64_t width, int64_t colAlign, int64_t colStride,
                      int64_t rowAlign, int64_t rowStride, const void* A, int64_t lda, void* portions,
