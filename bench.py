@@ -178,7 +178,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=["auto", "c2", "c3", "c4", "c5"], default="auto")
-    ap.add_argument("--n", type=int, default=0, help="override m=n=k (c2/c3/c5)")
+    ap.add_argument("--n", "--size", dest="n", type=int, default=0,
+                    help="override m=n=k (c2/c3/c5); --size under torch.distributed.run, whose parser takes --n")
     ap.add_argument("--dtype", choices=["f64", "f32", "bf16", "f16"], default=None)
     ap.add_argument("--nb", type=int, default=128, help="El::Blocksize (communication panel)")
     ap.add_argument("--kc", type=int, default=0, help="compute panel (0 = auto)")

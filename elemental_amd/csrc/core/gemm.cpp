@@ -446,14 +446,22 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             ELX_CHECK_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         }
     }
-    const int np = static_cast<int>((K + kc - 1) / kc);
+    // Panel p covers [kbeg(p), kbeg(p+1)).  On grids larger than 1x1 the first
+    // panel is a quarter of kc (whole communication panels): its gather is the
+    // one transfer no update hides, and the full-depth gather of panel 1 then
+    // runs behind panel 0's update (at 2x4, C3: ~30 ms of MFMA work against
+    // ~20 ms of transfer).  A 1x1 grid uses its panels in place: no ramp.
+    const Int nb = std::max<Int>(1, g_blocksize);
+    const Int kfirst = (g.Size() > 1 && kc >= 4 * nb && K > kc) ? std::max<Int>(nb, kc / 4 / nb * nb) : kc;
+    const int np = K == 0 ? 0 : K <= kfirst ? 1 : static_cast<int>(1 + (K - kfirst + kc - 1) / kc);
+    auto kbeg = [&](int p) { return p == 0 ? Int(0) : std::min<Int>(K, kfirst + Int(p - 1) * kc); };
     const int call_id = Prof().calls++;
     Buffer trrk_tmp;
 
     auto issue = [&](int p) {
         ELX_TRACE("SUMMA_C panel gather");
         Slot& s = slot[p & 1];
-        const Int k0 = p * kc, k1 = std::min(K, k0 + kc);
+        const Int k0 = kbeg(p), k1 = kbeg(p + 1);
         if (gpu && s.pending) ELX_CHECK_HIP(hipStreamWaitEvent(ms, s.done, 0));
         auto Av = IsN(oA) ? DistMatrix::View(A, 0, A.Height(), k0, k1) : DistMatrix::View(A, k0, k1, 0, A.Width());
         auto Bv = IsN(oB) ? DistMatrix::View(B, k0, k1, 0, B.Width()) : DistMatrix::View(B, 0, B.Height(), k0, k1);

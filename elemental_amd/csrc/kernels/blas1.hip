@@ -20,6 +20,7 @@
 #include "elem.hpp"
 #include "../../../include/elemental_amd.h"
 #include <algorithm>
+#include <cstdlib>
 #include <initializer_list>
 #include <utility>
 
@@ -322,6 +323,76 @@ __global__ __launch_bounds__(NT) void copy_cols_kernel(CopyBatch b, double alpha
     }
 }
 
+// Transposing moves with 16-B aligned unit-stride runs on both sides (the
+// `tvec` case of copy2d_kernel), without LDS: each lane owns R blocks of N x N
+// elements (N = 16 B / element, R = 16 / N, so 16 vectors in flight per lane),
+// reads each as N 16-B vectors along the source's unit-stride dimension,
+// transposes it in registers and writes N 16-B vectors along the
+// destination's.  A wave tile is 8N (source unit-stride) x 8NR elements: lane
+// (bu, bv) = (l & 7, l >> 3) owns the blocks (bu, bv + 8r), so every load and
+// every store instruction touches 8 full 128-B runs.  Wave tiles are dealt
+// over all waves of the grid; ragged ones move element by element.  For
+// 16-bit data this replaces 16 two-byte LDS accesses per 16 B moved.
+template <typename T, bool AXPY>
+__global__ __launch_bounds__(NT) void transpose_vec_kernel(CopyBatch b, double alpha) {
+    using E = Elem<T>;
+    using S = typename E::storage;
+    constexpr int N = V16<S>::N, R = 16 / N, WU = 8 * N, WV = 8 * N * R;
+    const Copy2D& d = b.d[blockIdx.y];
+    const S* src = static_cast<const S*>(d.src);
+    S* dst = static_cast<S*>(d.dst);
+    const bool src_i = d.scs == 1;  // source unit stride along i (then the destination's along j)
+    // (u, v) = (source unit-stride index, the other); element (u, v) of source / destination
+    const i64 su = src_i ? d.m : d.n, sv = src_i ? d.n : d.m;
+    const i64 s_v = src_i ? d.srs : d.scs;        // source stride of v
+    const i64 d_u = src_i ? d.dcs : d.drs;        // destination stride of u
+    const auto a = (typename E::compute)alpha;
+    const int l = threadIdx.x & 63, bu = l & 7, bv = l >> 3;
+    const i64 tu = (su + WU - 1) / WU, ntiles = tu * ((sv + WV - 1) / WV);
+    const i64 wave = (i64)blockIdx.x * (NT / 64) + (threadIdx.x >> 6), nwaves = (i64)gridDim.x * (NT / 64);
+    for (i64 t = wave; t < ntiles; t += nwaves) {
+        const i64 u0 = (t % tu) * WU, v0 = (t / tu) * WV;
+        if (u0 + WU <= su && v0 + WV <= sv) {
+            const i64 u = u0 + N * bu;
+            V16<S> x[R][N];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int e = 0; e < N; ++e)
+                    x[r][e] = *reinterpret_cast<const V16<S>*>(src + u + (v0 + N * (bv + 8 * r) + e) * s_v);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const i64 v = v0 + N * (bv + 8 * r);
+#pragma unroll
+                for (int g = 0; g < N; ++g) {
+                    V16<S>* o = reinterpret_cast<V16<S>*>(dst + v + (u + g) * d_u);
+                    V16<S> y;
+#pragma unroll
+                    for (int e = 0; e < N; ++e) y.v[e] = x[r][e].v[g];
+                    if (AXPY) {
+                        V16<S> z = *o;
+#pragma unroll
+                        for (int e = 0; e < N; ++e) z.v[e] = E::store(E::load(z.v[e]) + a * E::load(y.v[e]));
+                        *o = z;
+                    } else {
+                        *o = y;
+                    }
+                }
+            }
+        } else {
+            for (int q = l; q < WU * WV; q += 64) {
+                const i64 u = u0 + (q % WU), v = v0 + (q / WU);
+                if (u < su && v < sv) {
+                    const S xv = src[u + v * s_v];
+                    S* o = dst + v + u * d_u;
+                    if (AXPY) *o = E::store(E::load(*o) + a * E::load(xv));
+                    else *o = xv;
+                }
+            }
+        }
+    }
+}
+
 // 2-D elementwise driver (fill_hash): columns over gridDim.y, rows over gridDim.x*NT.
 template <typename F>
 __device__ __forceinline__ void for_each_2d(i64 m, i64 n, F&& f) {
@@ -500,15 +571,31 @@ dim3 grid2d(i64 m, i64 n) {
     default: return hipErrorInvalidValue;               \
     }
 
+// A transposing descriptor whose unit-stride runs are 16-B aligned on both
+// sides (the condition of copy2d_kernel's `tvec` branch): transpose_vec_kernel.
+bool TransposeVec(const Copy2D& x, int es) {
+    const bool src_i = x.scs == 1, dst_i = x.dcs == 1;
+    if (src_i == dst_i || (src_i ? false : x.srs != 1) || (dst_i ? false : x.drs != 1)) return false;
+    if (((reinterpret_cast<uintptr_t>(x.src) | reinterpret_cast<uintptr_t>(x.dst)) % 16) != 0) return false;
+    const i64 sother = src_i ? x.srs : x.scs, dother = dst_i ? x.drs : x.dcs;
+    return (sother * es) % 16 == 0 && (dother * es) % 16 == 0;
+}
+
+// ELX_TRANSPOSE_LDS=1: the LDS-tile transposition of copy2d_kernel for 16-bit data too (A/B timing)
+bool TransposeViaLds() {
+    static const bool v = [] { const char* e = getenv("ELX_TRANSPOSE_LDS"); return e && e[0] == '1'; }();
+    return v;
+}
+
 }  // namespace
 
 hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s) {
     for (int base = 0; base < nd; base += kMaxCopyBatch) {
         CopyBatch b{};
         const int cnt = (nd - base) < kMaxCopyBatch ? (nd - base) : kMaxCopyBatch;
-        i64 maxtiles = 0, maxvec = 0;
+        i64 maxtiles = 0, maxvec = 0, maxwt = 0;
         int used = 0;
-        bool cols = true;
+        bool cols = true, tvec_all = true;
         const int es = dtype == ELX_F64 ? 8 : dtype == ELX_F32 ? 4 : 2;
         for (int q = 0; q < cnt; ++q) {
             Copy2D x = d[base + q];
@@ -524,9 +611,23 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
             const i64 v = (x.m + 16 / es - 1) / (16 / es) * x.n;
             if (v > maxvec) maxvec = v;
             cols = cols && x.scs == 1 && x.dcs == 1;
+            tvec_all = tvec_all && TransposeVec(x, es);
+            const i64 w = 8 * (16 / es);  // wave tile: w x 128 elements
+            const i64 wt = ((x.m + w - 1) / w) * ((x.n + 127) / 128);
+            if (wt > maxwt) maxwt = wt;
         }
         if (used == 0) continue;
-        if (cols) {
+        // 16-bit: register blocks (4.08 vs 3.59 TB/s at 16384 x 8192); f32 / f64
+        // keep the LDS tile, which measured faster for them (4.71 vs 4.19, 5.04
+        // vs 4.93 TB/s; profiles/r02_transpose_ab.log)
+        if (!cols && tvec_all && es == 2 && !TransposeViaLds()) {
+            // ~8 workgroups per CU: 32 waves per CU over the batch's wave tiles
+            const unsigned gx = (unsigned)std::max<i64>(1, std::min<i64>((maxwt + 3) / 4, 2048));
+            dim3 grid(gx, used);
+            ELX_DTYPE_SWITCH(dtype, T,
+                if (axpy) hipLaunchKernelGGL((transpose_vec_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
+                else hipLaunchKernelGGL((transpose_vec_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
+        } else if (cols) {
             // ~16 workgroups per CU across the batch
             const i64 gx = std::max<i64>(1, std::min<i64>((maxvec + NT * UNROLL - 1) / (NT * UNROLL), 1 << 20));
             dim3 grid((unsigned)gx, used);

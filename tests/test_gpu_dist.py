@@ -87,6 +87,14 @@ def test_gpu_summa_multi_panel_distributed(world, height):
     _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130)], [el.GEMM_SUMMA_C], 16, 43, 16)
 
 
+@pytest.mark.parametrize("world,height", [(2, 1), (8, 2)])
+def test_gpu_summa_first_panel_ramp(world, height):
+    """Compute panel 64 = 4 x nb on a grid larger than 1x1: a 16-column first panel,
+    then 64-column panels (k = 130: 16, 64, 50; k = 80: 16, 64)."""
+    _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130), (33, 20, 80)], [el.GEMM_SUMMA_C], 16, 53,
+           64)
+
+
 @pytest.mark.parametrize("world,height,pool", [(1, 1, 2), (2, 1, 3), (4, 2, 2)])
 def test_gpu_summa_multistream(world, height, pool):
     """GEMM_SUMMA_{A,B,C}_MS with a stream pool (H_STREAMPOOL_SIZE = pool):

@@ -141,6 +141,37 @@ def _round(x, npdt):
 
 
 @pytest.mark.parametrize("t,npdt", DTYPES)
+@pytest.mark.parametrize("m,n,lda,ldb", [(200, 136, 208, 144), (64, 64, 64, 64), (512, 8, 520, 16), (256, 384, 264, 392)])
+def test_transpose_vectorized(t, npdt, m, n, lda, ldb):
+    """Transposing moves whose unit-stride runs are 16-B aligned on both sides
+    (transpose_vec_kernel: N x N register blocks, 8N x 8N wave tiles): whole and
+    ragged wave tiles, ld > height on both sides; copy (Transpose_GPU_impl) and
+    the transposed Axpy form (Axpy.cu:119-189), bit-exact."""
+    hostdt = np.uint16 if npdt == "bf16" else npdt
+    X = _mat(lda, n, 41, npdt)        # m x n view with ld = lda
+    B0 = _mat(ldb, m, 42, npdt)       # n x m view with ld = ldb
+    dX, dB = dev(X), dev(B0)
+    torch.cuda.synchronize()
+    L.call("elx_transpose", t, m, n, dX.data_ptr(), lda, dB.data_ptr(), ldb, None)
+    sync()
+    got = host(dB, (ldb, m), hostdt)
+    want = B0.copy()
+    want[:n, :] = X[:m, :].T
+    assert np.array_equal(got, want)
+    # W (n x m, ld ldb) += -2 X^T
+    W = _mat(ldb, m, 43, npdt)
+    dW = dev(W)
+    torch.cuda.synchronize()
+    L.call("elx_axpy2d", t, n, m, -2.0, dX.data_ptr(), lda, 1, dW.data_ptr(), 1, ldb, None)
+    sync()
+    cdt = np.float64 if t == L.F64 else np.float32
+    Wf, Xf = _as_f64(W, npdt), _as_f64(X, npdt)
+    wantW = W.copy()
+    wantW[:n, :] = _round(Wf[:n, :].astype(cdt) + cdt(-2.0) * Xf[:m, :].T.astype(cdt), npdt)
+    assert np.array_equal(host(dW, (ldb, m), hostdt), wantW)
+
+
+@pytest.mark.parametrize("t,npdt", DTYPES)
 def test_blas1_kernels(t, npdt):
     hostdt = np.uint16 if npdt == "bf16" else npdt
     m, n = 77, 45
