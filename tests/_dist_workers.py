@@ -800,3 +800,52 @@ def raw_coll_worker(rank: int, world: int, port: int):
     except Exception:
         traceback.print_exc()
         raise
+
+
+# tests/golden/mkl_summa.npz cases: dtype_grid_nb_mxnxk
+MKL_SUMMA = ["f64_2x2_nb16_45x37x61", "f64_1x2_nb8_30x41x27", "f64_2x4_nb16_53x66x130", "f64_2x2_nb128_260x200x300",
+             "f32_2x2_nb16_45x37x61", "f32_1x2_nb8_30x41x27", "f32_2x4_nb16_53x66x130", "f32_2x2_nb128_260x200x300"]
+
+
+def mkl_summa_worker(rank: int, world: int, port: int, height: int, device: int, keys):
+    """El::Gemm(NN, GEMM_SUMMA_C) with the fixture's Blocksize on its grid,
+    against the reference's SUMMA_NNC evaluated through MKL rank by rank
+    (tests/golden/mkl_summa.npz, tools/make_mkl_golden.py): each rank checks
+    its own local block with the north_star normwise bound (global norms)."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_summa.npz"))
+        for key in keys:
+            parts = key.split("_")
+            r, c = map(int, parts[1].split("x"))
+            if r * c != world:
+                continue
+            nb = int(parts[2][2:])
+            m, n, k = map(int, parts[3].split("x"))
+            dt = np.float64 if parts[0] == "f64" else np.float32
+            dtype = el.F64 if dt == np.float64 else el.F32
+            s = [int(x) for x in gold[key + "_seed"]]
+            Ag = oracle.hash_matrix(m, k, s[0], 0.0, 0.1, dt)
+            Bg = oracle.hash_matrix(k, n, s[1], 0.0, 0.1, dt)
+            Cg = oracle.hash_matrix(m, n, s[2], 0.0, 0.1, dt)
+            g = el.Grid(comm, r)
+            assert (g.height, g.width) == (r, c)
+            el.SetBlocksize(nb)
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=k)
+            B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=k, width=n)
+            C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
+            A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
+            B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
+            C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, el.GEMM_SUMMA_C)
+            got = C.get_local().astype(np.float64)
+            want = oracle.local_block(gold[key], el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
+            num = np.linalg.norm(got - want) if got.size else 0.0
+            den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) * k * np.finfo(dt).eps
+            assert np.isfinite(got).all() and num <= 10 * den, f"{key} rank {rank}: {num / den:.3g}"
+        el.SetBlocksize(128)
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise

@@ -163,3 +163,11 @@ def test_copy_type_conversion(world, height):
     """El::Copy between element types (CopyDistMatrix.hpp:28-57) on CPU matrices:
     all 12 ordered pairs of {f32, f64, f16, bf16}, bit-exact vs the oracle."""
     _spawn(W.convert_worker, world, height, el.CPU, 7)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_summa_matches_mkl_reference_path(world):
+    """The library's SUMMA_C on Device::CPU (gloo) against the reference CPU
+    path's own arithmetic: SUMMA_NNC evaluated rank by rank through MKL
+    2021.4.0 (tests/golden/mkl_summa.npz), 1x2 / 2x2 / 2x4 grids, f64 and f32."""
+    _spawn(W.mkl_summa_worker, world, 2 if world > 2 else 1, el.CPU, W.MKL_SUMMA)

@@ -209,6 +209,14 @@ def test_gpu_gemm_associativity_large(oA, oB):
     assert res < 1e-13, res  # reference measured 2.3e-16 at 4096
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gpu_summa_matches_mkl_reference_path(world):
+    """GPU SUMMA_C (host-staged panels, MFMA local updates) against the
+    reference CPU path's SUMMA_NNC evaluated through MKL rank by rank
+    (tests/golden/mkl_summa.npz): 1x2 / 2x2 / 2x4, f64 and f32, north_star bound."""
+    _spawn(W.mkl_summa_worker, world, 2 if world > 2 else 1, el.GPU, W.MKL_SUMMA)
+
+
 def _rccl_spawn(fn, world, *args):
     import os
     os.environ["ELX_TEST_BACKEND"] = "rccl"

@@ -140,6 +140,34 @@ def _round(x, npdt):
     return x.astype(npdt)
 
 
+def test_local_gemm_matches_mkl():
+    """elx_gemm_{f64,f32} (the MFMA kernels LocalGemm runs) against one MKL
+    dgemm_/sgemm_ call each (tests/golden/mkl_local.npz: the reference CPU
+    path's own BLAS at Gemm_impl<CPU>'s call site), all orientations, odd shapes."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_local.npz"))
+    keys = [k for k in d.files if k != "_mkl" and not k.endswith("_seed")]
+    assert len(keys) == 32
+    for key in keys:
+        tag, orient, shape = key.split("_")
+        dt = np.float64 if tag == "f64" else np.float32
+        ta, tb = orient[0], orient[1]
+        m, n, k = map(int, shape.split("x"))
+        s = [int(x) for x in d[key + "_seed"]]
+        A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, s[0], 0.0, 0.1, dt)
+        B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, s[1], 0.0, 0.1, dt)
+        C = oracle.hash_matrix(m, n, s[2], 0.0, 0.1, dt)
+        dA, dB, dC = dev(A), dev(B), dev(C)
+        torch.cuda.synchronize()
+        fn = "elx_gemm_f64" if tag == "f64" else "elx_gemm_f32"
+        L.call(fn, OPS[ta], OPS[tb], m, n, k, 0.5, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0], -0.5,
+               dC.data_ptr(), m, None)
+        sync()
+        got = host(dC, (m, n), dt)
+        r = oracle.parity_ratio(got, d[key], A, B, k, np.finfo(dt).eps)
+        assert r <= 10, (key, r)
+
+
 @pytest.mark.parametrize("t,npdt", DTYPES)
 @pytest.mark.parametrize("m,n,lda,ldb", [(200, 136, 208, 144), (64, 64, 64, 64), (512, 8, 520, 16), (256, 384, 264, 392)])
 def test_transpose_vectorized(t, npdt, m, n, lda, ldb):

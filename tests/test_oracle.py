@@ -180,3 +180,57 @@ def test_cpu_summa_baseline_small():
     from oracle import cpu_summa
     res = cpu_summa.run(n=256, nb=16, kc=64, r=2, c=2, seconds=0.2, cores=4)
     assert res["value"] > 0 and res["kind"] == "port" and res["cores"] == 4
+
+
+# ---- pinned to the reference CPU path's own BLAS (tools/make_mkl_golden.py) ----
+def _mkl_cases(name):
+    d = np.load(os.path.join(GOLD, name))
+    return d, [k for k in d.files if k != "_mkl" and not k.endswith("_seed")]
+
+
+def _mkl_inputs(d, key):
+    """(dtype, ta, tb, m, n, k, A, B, C) regenerated from the fixture's seeds."""
+    parts = key.split("_")
+    dt = np.float64 if parts[0] == "f64" else np.float32
+    m, n, k = map(int, parts[-1].split("x"))
+    ta, tb = (parts[1][0], parts[1][1]) if len(parts) == 3 else ("N", "N")
+    s = [int(x) for x in d[key + "_seed"]]
+    A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, s[0], 0.0, 0.1, dt)
+    B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, s[1], 0.0, 0.1, dt)
+    C = oracle.hash_matrix(m, n, s[2], 0.0, 0.1, dt)
+    return dt, ta, tb, m, n, k, A, B, C
+
+
+def test_oracle_matches_mkl_local_gemm():
+    """oracle.gemm (the restated loop nest of imports/blas/Gemm.hpp) against
+    one MKL dgemm_/sgemm_ call per case (MKL 2021.4.0, the reference CPU path's
+    BLAS): all four orientations, f64 and f32, within the north_star bound and
+    in fact well inside it (worst 0.22, the k = 5 case)."""
+    d, keys = _mkl_cases("mkl_local.npz")
+    assert "2021.4" in str(d["_mkl"][0]) and len(keys) == 32
+    worst = 0.0
+    for key in keys:
+        dt, ta, tb, m, n, k, A, B, C = _mkl_inputs(d, key)
+        ref = oracle.gemm(ta, tb, 0.5, A, B, -0.5, C)
+        r = oracle.parity_ratio(ref, d[key], A, B, k, np.finfo(dt).eps)
+        worst = max(worst, r)
+        assert r <= 10, (key, r)
+    assert worst < 1, worst
+
+
+def test_oracle_matches_mkl_summa():
+    """The oracle's simulated SUMMA_NNC and its plain GEMM against the
+    reference's SUMMA_NNC evaluated rank by rank through MKL (Scale(beta, C),
+    then one dgemm_('N','T') per Blocksize() panel per rank, NN.hpp:370-384)
+    on 2x2, 1x2 and 2x4 grids."""
+    d, keys = _mkl_cases("mkl_summa.npz")
+    assert len(keys) == 8
+    for key in keys:
+        dt, _, _, m, n, k, A, B, C = _mkl_inputs(d, key)
+        r_, c_ = map(int, key.split("_")[1].split("x"))
+        nb = int(key.split("_")[2][2:])
+        eps = np.finfo(dt).eps
+        assert oracle.parity_ratio(oracle.gemm("N", "N", 0.5, A, B, -0.5, C), d[key], A, B, k, eps) < 0.1, key
+        if dt == np.float64:
+            sim = oracle.summa_nnc(r_, c_, nb, 0.5, A, B, -0.5, C)
+            assert oracle.parity_ratio(sim, d[key], A, B, k, eps) < 0.1, key
