@@ -1014,7 +1014,8 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     const DistMatrix& A = *Ap;
     RWProxy Xp(XPre);
     DistMatrix& X = Xp.Get();
-    const Int m = X.Height(), n = X.Width(), nb = std::max<Int>(1, g_blocksize);
+    const Int m = X.Height(), n = X.Width();
+    Int nb = std::max<Int>(1, g_blocksize);
     const bool trans = orient != ELX_NORMAL, lower = uplo == ELX_LOWER;
     const bool forward = lower != trans;  // op(A) lower: blocks top to bottom
     auto A11s = A.Like(Dist::STAR, Dist::STAR);
@@ -1048,9 +1049,18 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     // elsewhere each block is solved where it lands (exec::Trsm)
     const size_t es = DTypeSize(X.Type());
     Buffer winv;
-    const bool batched = X.Dev() == Device::GPU && SameLocalLayout(A, Dist::STAR, Dist::STAR, 0, 0) &&
-                         nb * 65 * (Int)es <= 66 * 1024 && (m + nb - 1) / nb <= 65535 &&
-                         SameLocalLayout(X, Dist::STAR, Dist::VR, 0, X.RowAlign()) && X.LocalWidth() >= 4 * nb;
+    auto batch_ok = [&](Int b) {
+        return X.Dev() == Device::GPU && SameLocalLayout(A, Dist::STAR, Dist::STAR, 0, 0) &&
+               b * 65 * (Int)es <= kern::kTriInverseLdsMax && (m + b - 1) / b <= 65535 &&
+               SameLocalLayout(X, Dist::STAR, Dist::VR, 0, X.RowAlign()) && X.LocalWidth() >= 4 * b;
+    };
+    // Batched path with the default Blocksize (128) and a large system: 256-row
+    // diagonal blocks, so every leaf (inverse applied as a GEMM) and the lowest
+    // updates are 256 x n MFMA launches (256 output tiles, the whole machine)
+    // instead of 128 x n ones (half of it); ELX_TRSM_NB256=0 keeps 128.
+    static const bool nb256 = [] { const char* e = getenv("ELX_TRSM_NB256"); return !e || atoi(e) != 0; }();
+    if (nb256 && nb == 128 && m >= 8 * 256 && batch_ok(256)) nb = 256;
+    const bool batched = batch_ok(nb);
     std::shared_ptr<DistMatrix> Y;
     if (batched) {
         FenceStreams(A.Stream(), X.Stream());

@@ -100,6 +100,8 @@ hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, 
                       void* B, i64 ldb, hipStream_t s);
 // W_b := op(A_bb)^-1 for every nb x nb diagonal block of A (m x m; the last may be
 // ragged), W_b at W + b*nb*nb with leading dimension nb; one launch.  nb*65*es <= 66 KiB.
+// dynamic LDS of one tri_inverse_batched workgroup: nb x 65 elements
+constexpr long kTriInverseLdsMax = 150 * 1024;
 hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64 nb, i64 m, const void* A, i64 lda,
                                void* W, hipStream_t s);
 }  // namespace kern

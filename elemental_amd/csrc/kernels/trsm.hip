@@ -107,14 +107,20 @@ hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64
     const i64 nblk = (m + nb - 1) / nb;
     const int es = dtype == ELX_F64 ? 8 : 4;
     const size_t lds = (size_t)nb * (WAVE + 1) * es;
-    if (lds > 66 * 1024 || nblk > 65535) return hipErrorInvalidValue;
+    if (lds > (size_t)kTriInverseLdsMax || nblk > 65535) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((nb + WAVE - 1) / WAVE), (unsigned)nblk);
     switch (dtype) {
     case ELX_F64:
+        if (lds > 64 * 1024)  // beyond the default dynamic-LDS limit (gfx950: 160 KiB per workgroup)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<double>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL((tri_inverse_batched_kernel<double>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
                            static_cast<const double*>(A), lda, static_cast<double*>(W));
         break;
     case ELX_F32:
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<float>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL((tri_inverse_batched_kernel<float>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
                            static_cast<const float*>(A), lda, static_cast<float*>(W));
         break;

@@ -360,10 +360,12 @@ def test_gpu_trsm_distributed(world, height, flat, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [el.F64, el.F32])
-def test_gpu_trsm_large(dtype):
+@pytest.mark.parametrize("m,n", [(1500, 700), (2100, 1100)])
+def test_gpu_trsm_large(dtype, m, n):
     """1x1 grid, m = 1500 (12 blocks of 128, a ragged last one), 700 right-hand
-    sides: LEFT LOWER and UPPER, NORMAL and TRANSPOSE, against oracle.trsm."""
-    m, n = 1500, 700
+    sides; m = 2100, 1100 right-hand sides takes the 256-row diagonal blocks of
+    the batched path (ragged last block): LEFT LOWER and UPPER, NORMAL and
+    TRANSPOSE, against oracle.trsm."""
     npdt = np.float64 if dtype == el.F64 else np.float32
     g = el.Grid()
     el.SetBlocksize(128)
