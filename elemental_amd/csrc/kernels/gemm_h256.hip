@@ -501,6 +501,141 @@ __global__ __launch_bounds__(NT, 1) void gemm_h8b_kernel(H2Params p) {
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
+// ---------------------------------------------------------------------------
+// Deep-prefetch two-phase variant: the same tile, images and fragments, but each
+// K-tile runs as TWO phases of 32 MFMAs (phase h: the wave's rows {64h..64h+63}
+// x all 64 of its columns), so every barrier interval carries twice the MFMA
+// work of the phased kernels, and the B fragments are read once per K-tile and
+// kept for both phases.  Staging runs ~1.5 K-tiles ahead in the same two LDS
+// stages: the images of K-tile s that phase 0 reads (B0, B1, A0) are free once
+// phase 0's reads have retired, so K-tile s+2's B0, B1, A0 are staged into them
+// in phase 1 of s, and s+2's A1 in phase 0 of s+1 (into the slot K-tile s's A1
+// leaves when its phase-1 reads retire).  Per wave and phase: reads, staging,
+// `s_waitcnt vmcnt(8)` (the images read next were staged >= 3 intervals
+// earlier; the 8 youngest pieces may stay in flight), `lgkmcnt(0)` (every read
+// of this interval retired before the barrier, so the other group may restage
+// what it read: WAR), barrier, 32 MFMAs, barrier; the two wave groups one
+// barrier apart as in the phased kernels.
+// ---------------------------------------------------------------------------
+template <bool BF16>
+__device__ __forceinline__ void cluster32(f32x4 (&acc)[8][4], int h, const u32x4 (&a)[8], const u32x4 (&b)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[h * 4 + mi][ni] = mfma<BF16>(a[s * 4 + mi], b[s * 4 + ni], acc[h * 4 + mi][ni]);
+    __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ void wait_stage(bool deep) {
+    if (deep) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// phase 0 of K-tile t (in `cur`): B and A0 fragments read from cur, K-tile t+1's
+// A1 staged into `nxtA1` (t+1's stage), then the first 32 MFMAs
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__device__ __forceinline__ void phase0(const Frame& f, const lds_char* __restrict__ cur, lds_char* __restrict__ nxtA1,
+                                       i64 k1, bool st, bool deep, f32x4 (&acc)[8][4], u32x4 (&a)[8], u32x4 (&b)[8]) {
+    const int ar = f.wr * 64, bcol = f.wc * 32;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+                b[s * 4 + h * 2 + ni] = frag<KCB>(cur + (2 + h) * HALF, bcol + ni * 16, s, f.l);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) a[s * 4 + mi] = frag<KCA>(cur, ar + mi * 16, s, f.l);
+    if (st) stage_q<BUF, KCA>(f, 1, k1, nxtA1);
+    wait_stage(deep);
+    bar8();
+    cluster32<BF16>(acc, 0, a, b);
+    bar8();
+}
+
+// phase 1 of K-tile t: A1 fragments read from cur, K-tile t+2's B0, B1, A0 staged
+// into cur's (now free) slots, then the second 32 MFMAs
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__device__ __forceinline__ void phase1(const Frame& f, const lds_char* __restrict__ curA1, lds_char* __restrict__ curA0,
+                                       lds_char* __restrict__ curB, i64 k2, bool st, bool deep, f32x4 (&acc)[8][4],
+                                       u32x4 (&a)[8], const u32x4 (&b)[8]) {
+    const int ar = f.wr * 64;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) a[s * 4 + mi] = frag<KCA>(curA1, ar + mi * 16, s, f.l);
+    if (st) {
+        stage_q<BUF, KCB>(f, 2, k2, curB);
+        stage_q<BUF, KCB>(f, 3, k2, curB + HALF);
+        stage_q<BUF, KCA>(f, 0, k2, curA0);
+    }
+    wait_stage(deep);
+    bar8();
+    cluster32<BF16>(acc, 1, a, b);
+    bar8();
+}
+
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__global__ __launch_bounds__(NT, 1) void gemm_h4d_kernel(H2Params p) {
+    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    lds_char* lds = (lds_char*)lds_raw;
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    // prologue: K-tile 0 whole, K-tile 1's B0, B1, A0
+    stage_q<BUF, KCB>(f, 2, 0, lds + 2 * HALF);
+    stage_q<BUF, KCB>(f, 3, 0, lds + 3 * HALF);
+    stage_q<BUF, KCA>(f, 0, 0, lds);
+    stage_q<BUF, KCA>(f, 1, 0, lds + HALF);
+    if (nt > 1) {
+        stage_q<BUF, KCB>(f, 2, BK, lds + STAGE + 2 * HALF);
+        stage_q<BUF, KCB>(f, 3, BK, lds + STAGE + 3 * HALF);
+        stage_q<BUF, KCA>(f, 0, BK, lds + STAGE);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar8();
+    if (wr == 1) bar8();  // group 1 runs one barrier behind group 0
+    u32x4 a[8], b[8];
+    for (int t = 0; t < nt; t += 2) {
+        // K-tile t in stage 0, t+1 in stage 1 (the loop is unrolled by two so the
+        // stage pointers are compile-time offsets of the LDS base)
+        phase0<BF16, KCA, KCB, BUF>(f, lds, lds + STAGE + HALF, (i64)(t + 1) * BK, t + 1 < nt, t + 2 < nt, acc, a, b);
+        phase1<BF16, KCA, KCB, BUF>(f, lds + HALF, lds, lds + 2 * HALF, (i64)(t + 2) * BK, t + 2 < nt, t + 2 < nt, acc,
+                                    a, b);
+        if (t + 1 < nt) {
+            phase0<BF16, KCA, KCB, BUF>(f, lds + STAGE, lds + HALF, (i64)(t + 2) * BK, t + 2 < nt, t + 3 < nt, acc, a,
+                                        b);
+            phase1<BF16, KCA, KCB, BUF>(f, lds + STAGE + HALF, lds + STAGE, lds + STAGE + 2 * HALF, (i64)(t + 3) * BK,
+                                        t + 3 < nt, t + 3 < nt, acc, a, b);
+        }
+    }
+    if (wr == 0) bar8();  // matches group 1's last barrier
+
+    epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
+}
+
 // One 16 x 16 accumulator tile: rows i..i+15 (4 per lane), column j.
 template <bool BF16>
 __device__ __forceinline__ void epi_one(const H2Params& p, const f32x4 v4, i64 i, i64 j) {
@@ -564,17 +699,26 @@ hipError_t launch_p(const H2Params& p, hipStream_t s, int fl) {
     return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF>, p, s);
 }
 
-// Kernel choice (launch_h256): balanced-read (default), phased (ELX_H16_KERNEL=p), two-stage (=s);
+// Kernel choice (launch_h256): deep-prefetch two-phase (default, =d), balanced-read (=b),
+// phased (=p), two-stage (=s);
 // ELX_H16_FLAGS picks a timing ablation (profiles/r01_h16_ablation.log) of the
 // two-stage bf16 NN or phased bf16 TN kernel.
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h256(const H2Params& p, hipStream_t s) {
     static const int fl = [] { const char* v = getenv("ELX_H16_FLAGS"); return v ? atoi(v) : 0; }();
     static const bool two_stage = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 's'; }();
-    // default: the balanced-read kernel (+2-5 % over the phased kernel at 16384^3,
-    // profiles/r02_h16_experiments.log); ELX_H16_KERNEL=p the phased kernel (and
-    // its ablations), =s the two-stage kernel
-    static const bool balanced = [] { const char* v = getenv("ELX_H16_KERNEL"); return !v || v[0] == 'b'; }();
+    // ELX_H16_KERNEL=b: the balanced-read kernel (+2-5 % over the phased kernel at
+    // 16384^3, profiles/r02_h16_experiments.log); =p the phased kernel (and its
+    // ablations), =s the two-stage kernel
+    // default: the deep-prefetch two-phase kernel (+2-5 % over the balanced-read
+    // kernel on NN / TN / NT, C5 32768^3 1340 -> 1414 TF; profiles/r02_h16_deep.log)
+    static const bool balanced = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 'b'; }();
+    static const bool deep = [] { const char* v = getenv("ELX_H16_KERNEL"); return !v || v[0] == 'd'; }();
+    if (deep && fl == 0) {
+        if (dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2))
+            return launch(gemm_h4d_kernel<BF16, KCA, KCB, true>, p, s);
+        return launch(gemm_h4d_kernel<BF16, KCA, KCB, false>, p, s);
+    }
     if (balanced && fl == 0) {
         if (dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2))
             return launch(gemm_h8b_kernel<BF16, KCA, KCB, true>, p, s);
