@@ -172,6 +172,64 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
             "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3)}
 
 
+def config_one_gpu(el, L, grid, barrier, config: str, steps: int, warmup: int) -> dict:
+    """The other single-GPU BASELINE configs in the N=1 line (evidence beside the
+    driver's C2 value): C4, TN fp32 m=n=8192 k=524288 with [VC,STAR] inputs
+    (SUMMA_DOT, LBANN's weight-gradient shape), and C5, NN bf16 32768^3 on
+    [MC,MR] plus DistMatrix Axpy / Hadamard on the same operands."""
+    if config == "c4":
+        m = n = 8192
+        k = 524288
+        DT, dtype, oA = el.F32, "f32", el.TRANSPOSE
+        A = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
+        workload = "C4: El::Gemm TN f32 m=n=8192 k=524288 (SUMMA_DOT), A,B [VC,STAR], Grid 1x1"
+    else:
+        m = n = k = 32768
+        DT, dtype, oA = el.BF16, "bf16", el.NORMAL
+        A = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=k).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
+        workload = "C5: El::Gemm NN bf16 m=n=k=32768 on [MC,MR], Grid 1x1"
+    C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=n).fill_hash(3, 0.0, 0.1)
+    for _ in range(warmup):
+        el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
+    barrier()
+    L.call("elx_set_profiling", 1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = profile_summary(L, ctypes)
+    L.call("elx_set_profiling", 0)
+    value = 2.0 * m * n * k * steps / elapsed / 1e12
+    avg_ms = prof["gemm_ms"] / max(prof["launches"], 1)
+    fpl = prof["flops"] / max(prof["launches"], 1)
+    ach = fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    out = {"workload": workload, "value": round(value, 3), "unit": "TFLOP/s", "dtype": dtype, "steps": steps,
+           "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "pct_of_mfma_peak": round(100.0 * value / PEAK_TFLOPS[dtype], 2),
+           "roofline": {"bound": "mfma", "kernel": KERNEL[dtype], "achieved": round(ach, 3),
+                        "peak": PEAK_TFLOPS[dtype], "frac": round(ach / PEAK_TFLOPS[dtype], 4),
+                        "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)}}
+    if config == "c5":
+        loc = A.LocalHeight() * A.LocalWidth()
+        ew = {}
+        for name, fn in (("axpy", lambda: el.Axpy(0.5, A, C)), ("hadamard", lambda: el.Hadamard(A, B, C))):
+            fn()
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(20):
+                fn()
+            barrier()
+            dt = (time.perf_counter() - t1) / 20
+            gbs = 3 * 2 * loc / dt / 1e9
+            ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s": round(gbs, 1), "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+        out["entrywise"] = ew
+    del A, B, C
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +246,8 @@ def main():
     ap.add_argument("--c3-steps", type=int, default=2, help="timed steps of the N=1 C3 point")
     ap.add_argument("--no-c3-1gpu", action="store_true",
                     help="N=1: skip the same-problem C3 point (n=65536 through the panel path)")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="N=1: skip the C4 / C5 single-GPU points of the default line")
     args = ap.parse_args()
 
     import torch
@@ -382,6 +442,15 @@ def main():
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
         del A, B, C
         out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)
+    if world == 1 and config == "c2" and not args.n and not args.no_extra_configs:
+        # the other BASELINE configs that fit one GPU, measured in the same run
+        if "A" in locals():
+            del A, B, C
+        for cfg, st in (("c4", 2), ("c5", 5)):
+            try:
+                out[f"{cfg}_1gpu"] = config_one_gpu(el, L, grid, barrier, cfg, st, 1)
+            except Exception as e:  # evidence only: never lose the driver's line to it
+                out[f"{cfg}_1gpu"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
