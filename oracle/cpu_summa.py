@@ -38,7 +38,28 @@ def _port() -> int:
     return p
 
 
-def _worker(rank: int, world: int, port: int, r: int, n: int, nb: int, kc: int, seconds: float, threads: int, out):
+MKL_PATH = "/opt/conda/lib/libmkl_rt.so"  # the reference's BLAS in its documented build
+
+
+def _mkl_gemm(threads: int):
+    """dgemm_ of MKL 2021.4 (GNU OpenMP threading layer, as the reference's runs
+    require) with `threads` threads, or None when MKL is absent."""
+    if not os.path.exists(MKL_PATH):
+        return None
+    os.environ["MKL_THREADING_LAYER"] = "GNU"
+    lib = ctypes.CDLL(MKL_PATH)
+    lib.mkl_set_num_threads(ctypes.byref(ctypes.c_int(threads)))
+    i = lambda x: ctypes.byref(ctypes.c_int(int(x)))
+    d = lambda x: ctypes.byref(ctypes.c_double(x))
+
+    def gemm(m, n, k, alpha, A, lda, B, ldb, beta, C, ldc):
+        lib.dgemm_(ctypes.c_char_p(b"N"), ctypes.c_char_p(b"N"), i(m), i(n), i(k), d(alpha), A, i(lda), B, i(ldb),
+                   d(beta), C, i(ldc))
+    return gemm
+
+
+def _worker(rank: int, world: int, port: int, r: int, n: int, nb: int, kc: int, seconds: float, threads: int, out,
+            blas: str = "port"):
     os.environ["OMP_NUM_THREADS"] = str(threads)  # read by the OpenMP runtime when liboracle loads
     os.environ["OMP_WAIT_POLICY"] = "PASSIVE"     # idle workers must not spin on cores another rank computes on
     import torch
@@ -63,6 +84,9 @@ def _worker(rank: int, world: int, port: int, r: int, n: int, nb: int, kc: int, 
     L = oracle.lib()
     L.orc_cpu_set_threads(threads)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    mkl = _mkl_gemm(threads) if blas == "mkl" else None
+    if mkl is not None:
+        kc = nb  # the reference's own structure: one MKL update per Blocksize() panel (NN.hpp:373-384)
     alpha, beta = 0.5, -0.5
 
     A1 = np.empty((lh, kc), order="F")
@@ -88,7 +112,10 @@ def _worker(rank: int, world: int, port: int, r: int, n: int, nb: int, kc: int, 
                 B1[q0 + (i - k0) % r:q0 + nb:r, :] = gb[i].numpy()
             if q0 + nb == kc or k0 + nb == n:
                 kk = q0 + nb
-                L.orc_cpu_gemm_f64(b"N", b"N", lh, lw, kk, alpha, p(A1), lh, p(B1), kc, 1.0, p(C), lh)
+                if mkl is not None:
+                    mkl(lh, lw, kk, alpha, p(A1), lh, p(B1), kc, 1.0, p(C), lh)
+                else:
+                    L.orc_cpu_gemm_f64(b"N", b"N", lh, lw, kk, alpha, p(A1), lh, p(B1), kc, 1.0, p(C), lh)
 
     step()  # warm-up (thread pool, pages, gloo pairs)
     # correctness of a few entries against direct dot products of the global inputs
@@ -124,8 +151,10 @@ def _worker(rank: int, world: int, port: int, r: int, n: int, nb: int, kc: int, 
 
 
 def run(n: int = 4096, nb: int = 128, kc: int = 1024, r: int = 2, c: int = 2, seconds: float = 10.0,
-        cores: int = 0) -> dict:
-    """Time the CPU SUMMA on an r x c grid of processes; returns the cpu_baseline dict."""
+        cores: int = 0, blas: str = "auto") -> dict:
+    """Time the CPU SUMMA on an r x c grid of processes; returns the cpu_baseline dict.
+    blas: "mkl" local updates through MKL's dgemm_ per nb-panel (the reference's
+    BLAS and call structure), "port" through cpu_gemm.c, "auto" MKL when present."""
     import torch.multiprocessing as mp
 
     import oracle
@@ -137,8 +166,10 @@ def run(n: int = 4096, nb: int = 128, kc: int = 1024, r: int = 2, c: int = 2, se
     saved = {v: os.environ.get(v) for v in ("OMP_NUM_THREADS", "OMP_WAIT_POLICY")}
     os.environ["OMP_NUM_THREADS"] = str(threads)  # the children's OpenMP runtime reads it when it loads
     os.environ["OMP_WAIT_POLICY"] = "PASSIVE"
+    if blas == "auto":
+        blas = "mkl" if os.path.exists(MKL_PATH) else "port"
     try:
-        mp.spawn(_worker, args=(world, _port(), r, n, nb, kc, seconds, threads, q), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _port(), r, n, nb, kc, seconds, threads, q, blas), nprocs=world, join=True)
     finally:
         for v, x in saved.items():
             if x is None:
@@ -148,9 +179,11 @@ def run(n: int = 4096, nb: int = 128, kc: int = 1024, r: int = 2, c: int = 2, se
     steps, elapsed = q.get()
     return {"value": round(2.0 * n ** 3 * steps / elapsed / 1e12, 4), "unit": "TFLOP/s", "cores": threads * world,
             "kind": "port",
-            "sample": f"C1: CPU SUMMA_NNC NN f64 m=n=k={n}, nb={nb} panels gathered, local update every {kc} columns, "
-                      f"{r}x{c} grid of {world} processes x {threads} "
-                      f"OpenMP threads (oracle/cpu_summa.py: gloo all-gathers + cpu_gemm.c blocked dgemm), "
+            "blas": "MKL 2021.4 dgemm_ (the reference's BLAS)" if blas == "mkl" else "cpu_gemm.c",
+            "sample": f"C1: CPU SUMMA_NNC NN f64 m=n=k={n}, nb={nb} panels gathered, local update every "
+                      f"{nb if blas == 'mkl' else kc} columns, {r}x{c} grid of {world} processes x {threads} "
+                      f"threads (oracle/cpu_summa.py: gloo all-gathers + "
+                      f"{'MKL 2021.4 dgemm_, GNU threading layer' if blas == 'mkl' else 'cpu_gemm.c blocked dgemm'}), "
                       f"{steps} steps in {elapsed:.1f} s; the reference measured 0.288 s/step (477 GFLOP/s) "
                       f"on 8 cores, BASELINE.md §2"}
 
