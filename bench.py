@@ -172,24 +172,27 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
             "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3)}
 
 
-def config_one_gpu(el, L, grid, barrier, config: str, steps: int, warmup: int) -> dict:
-    """The other single-GPU BASELINE configs in the N=1 line (evidence beside the
-    driver's C2 value): C4, TN fp32 m=n=8192 k=524288 with [VC,STAR] inputs
-    (SUMMA_DOT, LBANN's weight-gradient shape), and C5, NN bf16 32768^3 on
-    [MC,MR] plus DistMatrix Axpy / Hadamard on the same operands."""
+def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: int, world: int, size: int = 0) -> dict:
+    """The other BASELINE configs as sub-results of the default line (evidence
+    beside the driver's C2 / C3 value, measured in the same run on the same
+    grid): C4, TN fp32 m=n=8192 k=524288*N with [VC,STAR] inputs (SUMMA_DOT,
+    LBANN's weight-gradient shape; weak scaling, = C4 at N=8), and C5, NN bf16
+    32768^3 on [MC,MR] plus DistMatrix Axpy / Hadamard on the same operands.
+    size > 0 (rehearsals only): m = n = min(8192, size), k = size*N for C4, n = size for C5."""
+    gshape = f"{grid.height}x{grid.width}"
     if config == "c4":
-        m = n = 8192
-        k = 524288
+        m = n = min(8192, size) if size else 8192
+        k = (size or 524288) * world
         DT, dtype, oA = el.F32, "f32", el.TRANSPOSE
         A = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
         B = el.DistMatrix(grid, DT, el.VC, el.STAR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
-        workload = "C4: El::Gemm TN f32 m=n=8192 k=524288 (SUMMA_DOT), A,B [VC,STAR], Grid 1x1"
+        workload = f"C4: El::Gemm TN f32 m=n={m} k={k} (SUMMA_DOT), A,B [VC,STAR], Grid {gshape}"
     else:
-        m = n = k = 32768
+        m = n = k = size or 32768
         DT, dtype, oA = el.BF16, "bf16", el.NORMAL
         A = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=k).fill_hash(1, 0.0, 0.1)
         B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
-        workload = "C5: El::Gemm NN bf16 m=n=k=32768 on [MC,MR], Grid 1x1"
+        workload = f"C5: El::Gemm NN bf16 m=n=k={m} on [MC,MR], Grid {gshape}"
     C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=n).fill_hash(3, 0.0, 0.1)
     for _ in range(warmup):
         el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
@@ -199,7 +202,7 @@ def config_one_gpu(el, L, grid, barrier, config: str, steps: int, warmup: int) -
     for _ in range(steps):
         el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = maxr(time.perf_counter() - t0)
     prof = profile_summary(L, ctypes)
     L.call("elx_set_profiling", 0)
     value = 2.0 * m * n * k * steps / elapsed / 1e12
@@ -208,10 +211,12 @@ def config_one_gpu(el, L, grid, barrier, config: str, steps: int, warmup: int) -
     ach = fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     out = {"workload": workload, "value": round(value, 3), "unit": "TFLOP/s", "dtype": dtype, "steps": steps,
            "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
-           "pct_of_mfma_peak": round(100.0 * value / PEAK_TFLOPS[dtype], 2),
+           "pct_of_mfma_peak": round(100.0 * value / (PEAK_TFLOPS[dtype] * world), 2),
            "roofline": {"bound": "mfma", "kernel": KERNEL[dtype], "achieved": round(ach, 3),
                         "peak": PEAK_TFLOPS[dtype], "frac": round(ach / PEAK_TFLOPS[dtype], 4),
                         "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)}}
+    if world > 1:
+        out["collectives"] = collectives_summary(prof, steps)
     if config == "c5":
         loc = A.LocalHeight() * A.LocalWidth()
         ew = {}
@@ -222,9 +227,10 @@ def config_one_gpu(el, L, grid, barrier, config: str, steps: int, warmup: int) -
             for _ in range(20):
                 fn()
             barrier()
-            dt = (time.perf_counter() - t1) / 20
+            dt = maxr((time.perf_counter() - t1) / 20)
             gbs = 3 * 2 * loc / dt / 1e9
-            ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s": round(gbs, 1), "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+            ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
+                        "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
         out["entrywise"] = ew
     del A, B, C
     return out
@@ -442,15 +448,17 @@ def main():
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
         del A, B, C
         out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)
-    if world == 1 and config == "c2" and not args.n and not args.no_extra_configs:
-        # the other BASELINE configs that fit one GPU, measured in the same run
+    if config in ("c2", "c3") and (not args.n or rehearse) and not args.no_extra_configs:
+        # the other BASELINE configs, measured in the same run on the same grid
+        # (N = 1: c4_1gpu / c5_1gpu; N > 1: c4 / c5 on Grid::DefaultHeight(N))
         if "A" in locals():
             del A, B, C
         for cfg, st in (("c4", 2), ("c5", 5)):
+            key = f"{cfg}_1gpu" if world == 1 else cfg
             try:
-                out[f"{cfg}_1gpu"] = config_one_gpu(el, L, grid, barrier, cfg, st, 1)
+                out[key] = config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1, world, args.n)
             except Exception as e:  # evidence only: never lose the driver's line to it
-                out[f"{cfg}_1gpu"] = {"error": str(e)}
+                out[key] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
