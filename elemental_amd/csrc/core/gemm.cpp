@@ -136,6 +136,14 @@ std::shared_ptr<const DistMatrix> ReadProxy(const DistMatrix& A, const DistMatri
     }
     auto T = A.LikeOn(cd, rd, tgt.Dev());
     T->SetStream(tgt.Stream());
+    // A's local block already holds exactly the (cd,rd) block on every rank
+    // (e.g. [MC,MR] -> [VC,*] on a 1x1 grid): relabel it in place, no copy
+    const int ca = calign >= 0 ? calign : 0, ra = ralign >= 0 ? ralign : 0;
+    if (A.Dev() == tgt.Dev() && A.Root() == 0 && SameLocalLayout(A, cd, rd, ca, ra)) {
+        T->Attach(A.Height(), A.Width(), ca, ra, const_cast<void*>(A.Buffer()), A.LDim(), 0);
+        if (A.Dev() == Device::GPU) FenceStreams(A.Stream(), tgt.Stream());
+        return T;
+    }
     if (calign >= 0) T->AlignCols(calign, true);
     if (ralign >= 0) T->AlignRows(ralign, true);
     Copy(A, *T);
