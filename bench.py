@@ -446,13 +446,12 @@ def main():
     if world == 1 and config == "c2" and not args.n and not args.no_c3_1gpu:
         # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 8192
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
-        del A, B, C
+        A = B = C = None  # release the C2 operands before the n = 65536 ones
         out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)
     if config in ("c2", "c3") and (not args.n or rehearse) and not args.no_extra_configs:
         # the other BASELINE configs, measured in the same run on the same grid
         # (N = 1: c4_1gpu / c5_1gpu; N > 1: c4 / c5 on Grid::DefaultHeight(N))
-        if "A" in locals():
-            del A, B, C
+        A = B = C = None  # release the main operands (no-op when already released)
         for cfg, st in (("c4", 2), ("c5", 5)):
             key = f"{cfg}_1gpu" if world == 1 else cfg
             try:
