@@ -2,6 +2,7 @@
 Device::GPU matrices.  Multi-rank cases run 2 or 4 processes on the one GPU of
 the box with a host-staged (gloo) comm, so the device pack/unpack kernels,
 panel pipeline and MFMA updates run for real on every rank."""
+import os
 import socket
 
 import numpy as np
@@ -186,6 +187,48 @@ def test_gpu_summa_pipeline_multi_panel():
     Ag, Bg, Cg = (oracle.hash_matrix(*s, seed, -0.1, 0.1) for s, seed in (((m, k), 1), ((k, n), 2), ((m, n), 3)))
     ref = oracle.gemm("N", "N", 0.5, Ag, Bg, -0.5, Cg)
     assert oracle.parity_ratio(got, ref, Ag, Bg, k, np.finfo(np.float64).eps) <= 10
+
+
+_COPIED_PANELS = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle
+from elemental_amd import el
+m, n, k = 1300, 1100, 2100
+g = el.Grid()
+el.SetBlocksize(128)
+el.SetComputePanel(256)
+for oA in (el.NORMAL, el.TRANSPOSE):
+    for oB in (el.NORMAL, el.TRANSPOSE):
+        sa = (m, k) if oA == el.NORMAL else (k, m)
+        sb = (k, n) if oB == el.NORMAL else (n, k)
+        A = el.DistMatrix(g, el.F64, height=sa[0], width=sa[1]).fill_hash(1, -0.1, 0.1)
+        B = el.DistMatrix(g, el.F64, height=sb[0], width=sb[1]).fill_hash(2, -0.1, 0.1)
+        C = el.DistMatrix(g, el.F64, height=m, width=n).fill_hash(3, -0.1, 0.1)
+        el.Gemm(oA, oB, 0.5, A, B, -0.5, C, el.GEMM_SUMMA_C)
+        got = C.get_local()
+        Ag, Bg, Cg = (oracle.hash_matrix(*sh, seed, -0.1, 0.1) for sh, seed in ((sa, 1), (sb, 2), ((m, n), 3)))
+        ref = oracle.gemm("NT"[oA], "NT"[oB], 0.5, Ag, Bg, -0.5, Cg)
+        r = oracle.parity_ratio(got, ref, Ag, Bg, k, np.finfo(np.float64).eps)
+        assert r <= 10, (oA, oB, r)
+print("ok")
+"""
+
+
+def test_gpu_summa_pipeline_copied_panels():
+    """ELX_SUMMA_COPY=1 (a child process: the knob is read once): every panel of
+    a 1x1 SUMMA_C is COPIED into the two slots on the comm stream while the MFMA
+    kernels read the other slot - the N > 1 pipeline's stream pattern and
+    write-after-read fences with the LDS-DMA kernels at full tile counts
+    (9 panels of 256, all four orientations), against the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ELX_SUMMA_COPY="1")
+    out = subprocess.run([sys.executable, "-c", _COPIED_PANELS, root], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stdout + out.stderr
 
 
 @pytest.mark.parametrize("oA,oB", [(0, 0), (0, 1), (1, 0), (1, 1)])
