@@ -428,6 +428,24 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
     const Dist a_cd = IsN(oA) ? Dist::MC : Dist::STAR, a_rd = IsN(oA) ? Dist::STAR : Dist::MC;
     const Dist b_cd = IsN(oB) ? Dist::STAR : Dist::MR, b_rd = IsN(oB) ? Dist::MR : Dist::STAR;
 
+    // One rank and one compute panel: the whole product is ONE local update with
+    // beta folded in (no panel slots, comm-stream fences or events; saves ~45 us
+    // of host work per call, which is most of a 1024^3 call)
+    if (g.Size() == 1 && uplo < 0 && K > 0 && kc >= K) {
+        const Int m = C.LocalHeight(), n = C.LocalWidth();
+        if (m > 0 && n > 0) {
+            const bool prof = gpu && Prof().on;
+            const int call_id = Prof().calls++;
+            Profiler::Rec rec{};
+            if (prof) rec = Prof().Begin(cs);
+            exec::Gemm(dev, C.Type(), !IsN(oA), !IsN(oB), m, n, K, alpha, A.Buffer(), A.LDim(), B.Buffer(), B.LDim(),
+                       beta, C.Buffer(), C.LDim(), cs);
+            if (prof) Prof().End(rec, cs, 2.0 * m * n * K, Prof().gemm, call_id);
+        }
+        Cp.Finish();
+        return;
+    }
+
     // inputs (and beta*C) must be complete before the comm stream reads them
     if (gpu) {
         FenceStreams(A.Stream(), ms);

@@ -32,9 +32,13 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
         d.kchunk = d.kmain;
         return d;
     }
-    // few tiles: split k into chunks of >= 2048 (whole slabs) for two rounds of workgroups
+    // few tiles: split k for two rounds of workgroups, in chunks of >= 2048 (whole
+    // slabs); with fewer tiles than CUs, chunks down to 256 (1024^3 f64: 64 tiles
+    // -> 4 chunks, 150 -> 60 us; at 2048^3, 256 tiles, chunks of 512 measured
+    // slower than none: the partials' HBM round trip outweighs the fill)
+    const i64 min_chunk = tiles < 256 ? 256 : 2048;
     i64 z = (2 * slots + tiles - 1) / tiles;
-    z = z < d.kmain / 2048 ? z : d.kmain / 2048;
+    z = z < d.kmain / min_chunk ? z : d.kmain / min_chunk;
     z = z < 16 ? z : 16;
     if (z < 2) {
         // k too short to split: the DMA kernel on the few tiles there are, or
