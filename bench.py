@@ -458,6 +458,24 @@ def main():
                 out[key] = config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1, world, args.n)
             except Exception as e:  # evidence only: never lose the driver's line to it
                 out[key] = {"error": str(e)}
+    if world == 1 and config == "c2" and not args.n and not args.no_extra_configs:
+        # C1's problem (NN f64 4096^3) on the GPU, beside the CPU leg's same problem
+        n1 = 4096
+        A1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(1, 0.0, 0.1)
+        B1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(2, 0.0, 0.1)
+        C1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(3, 0.0, 0.1)
+        for _ in range(3):
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
+        barrier()
+        dt = (time.perf_counter() - t1) / 20
+        out["c1_1gpu"] = {"workload": "C1's problem on the GPU: El::Gemm NN f64 m=n=k=4096, Grid 1x1",
+                          "value": round(2.0 * n1 ** 3 / dt / 1e12, 3), "unit": "TFLOP/s", "steps": 20,
+                          "ms_per_step": round(dt * 1e3, 3)}
+        del A1, B1, C1
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
