@@ -55,10 +55,23 @@ __device__ __forceinline__ void trsm_body(bool lower, bool trans, bool unit, i64
         T xi = X(i);
         if (!unit) xi = xi / (LDS ? acol[i] : opA(i, i));
         X(i) = xi;
-        if (forward)
-            for (i64 r = i + 1; r < m; ++r) X(r) = X(r) - (LDS ? acol[r] : opA(r, i)) * xi;
-        else
-            for (i64 r = 0; r < i; ++r) X(r) = X(r) - (LDS ? acol[r] : opA(r, i)) * xi;
+        // rows [r0, r1) -= op(A)(r, i) x_i, eight rows per batch: all sixteen
+        // loads issued before the first FMA (one LDS latency per batch, not per row)
+        const i64 r0 = forward ? i + 1 : 0, r1 = forward ? m : i;
+        i64 r = r0;
+        if (LDS) {
+            for (; r + 8 <= r1; r += 8) {
+                T xv[8], av[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    xv[u] = X(r + u);
+                    av[u] = acol[r + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) X(r + u) = xv[u] - av[u] * xi;
+            }
+        }
+        for (; r < r1; ++r) X(r) = X(r) - (LDS ? acol[r] : opA(r, i)) * xi;
     }
     if (LDS && live)
         for (i64 r = 0; r < m; ++r) bcol[r] = x[r * WAVE + threadIdx.x];
