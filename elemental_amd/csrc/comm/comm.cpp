@@ -342,6 +342,41 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
     }
 }
 
+void Comm::AllToAllVGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s) {
+    if (sets.size() == 1 || kind_ != Kind::RCCL || size_ == 1) {
+        for (const VSet& v : sets) AllToAllV(v.t, v.send, *v.sc, *v.sd, v.recv, *v.rc, *v.rd, dev, s);
+        return;
+    }
+    ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+    auto& st = GlobalCommStats();
+    int64_t in_bytes = 0;
+    for (const VSet& v : sets) {
+        const size_t es = DTypeSize(v.t);
+        st.calls++;
+        for (int q = 0; q < size_; ++q)
+            if (q != rank_) in_bytes += static_cast<int64_t>((*v.rc)[q] * es);
+        // the self portion never leaves the device
+        CopyBytes(dev, static_cast<char*>(v.recv) + (*v.rd)[rank_] * es,
+                  static_cast<const char*>(v.send) + (*v.sd)[rank_] * es, static_cast<size_t>((*v.rc)[rank_]) * es, s);
+    }
+    st.bytes += in_bytes;
+    auto rec = CommProf().Begin(s);
+    CheckNccl(ncclGroupStart(), "ncclGroupStart");
+    for (const VSet& v : sets) {
+        const size_t es = DTypeSize(v.t);
+        const ncclDataType_t nt = NcclType(v.t);
+        const char* sb = static_cast<const char*>(v.send);
+        char* rb = static_cast<char*>(v.recv);
+        for (int q = 0; q < size_; ++q) {
+            if (q == rank_) continue;
+            if ((*v.sc)[q] > 0) CheckNccl(ncclSend(sb + (*v.sd)[q] * es, (*v.sc)[q], nt, q, nccl_, s), "ncclSend");
+            if ((*v.rc)[q] > 0) CheckNccl(ncclRecv(rb + (*v.rd)[q] * es, (*v.rc)[q], nt, q, nccl_, s), "ncclRecv");
+        }
+    }
+    CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+    CommProf().End(rec, s, in_bytes);
+}
+
 void Comm::SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s) {
     const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
     ELX_REQUIRE(dest >= 0 && dest < size_ && src >= 0 && src < size_, "SendRecv: bad peer ", dest, "/", src, " of ",

@@ -71,6 +71,19 @@ public:
     void AllToAllV(DType t, const void* send, const std::vector<Int>& scounts, const std::vector<Int>& sdispls,
                    void* recv, const std::vector<Int>& rcounts, const std::vector<Int>& rdispls, Device dev,
                    hipStream_t s);
+    // Several AllToAllV exchanges of one communicator in ONE RCCL group (every
+    // set's sends and receives posted together, so exchanges with disjoint peer
+    // sets use their links concurrently); other backends run them in order.
+    struct VSet {
+        DType t;
+        const void* send;
+        const std::vector<Int>* sc;
+        const std::vector<Int>* sd;
+        void* recv;
+        const std::vector<Int>* rc;
+        const std::vector<Int>* rd;
+    };
+    void AllToAllVGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s);
     // Point-to-point exchange (El::mpi::SendRecv, src/core/imports/mpi/SendRecv.hpp:9-60):
     // send `count` elements to `dest` while receiving `count` from `src`.
     void SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s);

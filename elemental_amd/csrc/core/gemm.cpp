@@ -501,11 +501,16 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         // panel on a 1x1 grid) is used in place: no copy at all (ELX_SUMMA_COPY=1
         // copies anyway: the N > 1 pipeline's stream pattern on one GPU, for tests
         // and timing studies)
+        // The A and B gathers share ONE grouped exchange: they reach disjoint
+        // peers (the grid row and the grid column), so their xGMI links carry
+        // them concurrently instead of one after the other
         static const bool force_copy = [] { const char* e = getenv("ELX_SUMMA_COPY"); return e && atoi(e) > 0; }();
+        std::vector<std::pair<const DistMatrix*, DistMatrix*>> gathers;
         if (!force_copy && SameLocalLayout(*Av, a_cd, a_rd, s.a->ColAlign(), s.a->RowAlign())) s.ua = Av;
-        else { Copy(*Av, *s.a); s.ua = s.a; }
+        else { gathers.push_back({Av.get(), s.a.get()}); s.ua = s.a; }
         if (!force_copy && SameLocalLayout(*Bv, b_cd, b_rd, s.b->ColAlign(), s.b->RowAlign())) s.ub = Bv;
-        else { Copy(*Bv, *s.b); s.ub = s.b; }
+        else { gathers.push_back({Bv.get(), s.b.get()}); s.ub = s.b; }
+        CopyGroup(gathers);
         if (prof) Prof().End(rec, ms, static_cast<double>(GlobalCommStats().bytes - bytes0), Prof().comm);
         if (gpu) ELX_CHECK_HIP(hipEventRecord(s.ready, ms));
     };

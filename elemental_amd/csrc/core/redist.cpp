@@ -157,8 +157,24 @@ std::shared_ptr<DistMatrix> OnDevice(const DistMatrix& A, Device dev, hipStream_
 }
 
 // Shared transfer for Copy (designated senders, overwrite) and AxpyContract
-// (every owner sends, receiver sums in rank order).
-void Transfer(const DistMatrix& A, DistMatrix& B, bool contract, double alpha) {
+// (every owner sends, receiver sums in rank order), in three stages so several
+// transfers can share one exchange (CopyGroup): Prepare (plans, buffers, pack
+// and the local portion, on B's stream), the AllToAllV over the VC
+// communicator, Finish (unpack / rank-ordered sums).
+struct TransferJob {
+    const DistMatrix* A;
+    DistMatrix* B;
+    bool contract;
+    double alpha;
+    std::vector<PairPlan> out, in;
+    std::vector<Int> sc, sd, rc, rd;
+    bool cross = false;  // does any rank exchange data with another? (same answer on every rank)
+    elx::Buffer sbuf, rbuf;
+};
+
+void TransferPrepare(TransferJob& j) {
+    const DistMatrix& A = *j.A;
+    DistMatrix& B = *j.B;
     const Grid& g = A.G();
     const int p = g.Size(), me = g.VCRank();
     const DType t = A.Type();
@@ -167,78 +183,94 @@ void Transfer(const DistMatrix& A, DistMatrix& B, bool contract, double alpha) {
     hipStream_t st = B.Stream();
     Fence(A, B);
 
-    auto sends_to = [&](int s, int d) { return contract ? A.ParticipatingOf(s) : Designated(A, s, d); };
+    auto sends_to = [&](int s, int d) { return j.contract ? A.ParticipatingOf(s) : Designated(A, s, d); };
+    for (int s = 0; s < p && !j.cross; ++s)
+        for (int d = 0; d < p && !j.cross; ++d)
+            if (s != d && sends_to(s, d) && Plan(A, B, s, d).count() > 0) j.cross = true;
 
-    bool cross = false;  // does any rank exchange data with another? (same answer on every rank)
-    for (int s = 0; s < p && !cross; ++s)
-        for (int d = 0; d < p && !cross; ++d)
-            if (s != d && sends_to(s, d) && Plan(A, B, s, d).count() > 0) cross = true;
-
-    std::vector<PairPlan> out(p), in(p);
-    std::vector<Int> sc(p, 0), sd(p, 0), rc(p, 0), rd(p, 0);
+    j.out.assign(p, PairPlan{});
+    j.in.assign(p, PairPlan{});
+    j.sc.assign(p, 0); j.sd.assign(p, 0); j.rc.assign(p, 0); j.rd.assign(p, 0);
     Int stot = 0, rtot = 0;
     for (int q = 0; q < p; ++q) {
-        if (sends_to(me, q)) out[q] = Plan(A, B, me, q);
-        if (sends_to(q, me)) in[q] = Plan(A, B, q, me);
+        if (sends_to(me, q)) j.out[q] = Plan(A, B, me, q);
+        if (sends_to(q, me)) j.in[q] = Plan(A, B, q, me);
         if (q == me) continue;
-        sc[q] = out[q].count(); sd[q] = stot; stot += sc[q];
-        rc[q] = in[q].count();  rd[q] = rtot; rtot += rc[q];
+        j.sc[q] = j.out[q].count(); j.sd[q] = stot; stot += j.sc[q];
+        j.rc[q] = j.in[q].count();  j.rd[q] = rtot; rtot += j.rc[q];
     }
-
-    // the local portion moves directly (never through the send buffer)
-    auto local_desc = [&](const PairPlan& pl) {
-        return kern::Copy2D{pl.rows.count, pl.cols.count,
-                            At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step, pl.cols.src_step * A.LDim(),
-                            At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step, pl.cols.dst_step * B.LDim()};
-    };
-
-    elx::Buffer sbuf, rbuf;
-    if (cross) {
-        sbuf.Reset(dev, static_cast<size_t>(stot) * es, st);
-        rbuf.Reset(dev, static_cast<size_t>(rtot) * es, st);
+    if (j.cross) {
+        j.sbuf.Reset(dev, static_cast<size_t>(stot) * es, st);
+        j.rbuf.Reset(dev, static_cast<size_t>(rtot) * es, st);
         std::vector<kern::Copy2D> pack;
         for (int q = 0; q < p; ++q) {
-            if (q == me || sc[q] == 0) continue;
-            const PairPlan& pl = out[q];
+            if (q == me || j.sc[q] == 0) continue;
+            const PairPlan& pl = j.out[q];
             pack.push_back({pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
-                            pl.cols.src_step * A.LDim(), static_cast<char*>(sbuf.data()) + sd[q] * es, 1,
+                            pl.cols.src_step * A.LDim(), static_cast<char*>(j.sbuf.data()) + j.sd[q] * es, 1,
                             pl.rows.count});
         }
         exec::Copy2DBatch(dev, t, pack.data(), static_cast<int>(pack.size()), false, 0.0, st);
     }
-    if (!contract && out[me].count() > 0) {
-        auto d = local_desc(out[me]);
+    // the local portion moves directly (never through the send buffer)
+    if (!j.contract && j.out[me].count() > 0) {
+        const PairPlan& pl = j.out[me];
+        kern::Copy2D d{pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
+                       pl.cols.src_step * A.LDim(), At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
+                       pl.cols.dst_step * B.LDim()};
         exec::Copy2DBatch(dev, t, &d, 1, false, 0.0, st);
     }
-    if (cross) g.VC().AllToAllV(t, sbuf.data(), sc, sd, rbuf.data(), rc, rd, dev, st);
+}
 
+void TransferFinish(TransferJob& j) {
+    const DistMatrix& A = *j.A;
+    DistMatrix& B = *j.B;
+    const int p = A.G().Size(), me = A.G().VCRank();
+    const DType t = A.Type();
+    const Device dev = B.Dev();
+    const size_t es = A.ElemSize();
+    hipStream_t st = B.Stream();
     auto unpack_desc = [&](int q) {
-        const PairPlan& pl = in[q];
-        return kern::Copy2D{pl.rows.count, pl.cols.count, static_cast<char*>(rbuf.data()) + rd[q] * es, 1,
+        const PairPlan& pl = j.in[q];
+        return kern::Copy2D{pl.rows.count, pl.cols.count, static_cast<char*>(j.rbuf.data()) + j.rd[q] * es, 1,
                             pl.rows.count, At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
                             pl.cols.dst_step * B.LDim()};
     };
-    if (!contract) {
+    if (!j.contract) {
         std::vector<kern::Copy2D> unpack;
         for (int q = 0; q < p; ++q)
-            if (q != me && rc[q] > 0) unpack.push_back(unpack_desc(q));
+            if (q != me && j.rc[q] > 0) unpack.push_back(unpack_desc(q));
         exec::Copy2DBatch(dev, t, unpack.data(), static_cast<int>(unpack.size()), false, 0.0, st);
     } else {
         // sum contributions in rank order (deterministic); one launch per source
         // so two sources never update the same element concurrently
         for (int q = 0; q < p; ++q) {
             if (q == me) {
-                if (in[me].count() > 0) {
-                    auto d = local_desc(in[me]);
-                    exec::Copy2DBatch(dev, t, &d, 1, true, alpha, st);
+                if (j.in[me].count() > 0) {
+                    const PairPlan& pl = j.in[me];
+                    kern::Copy2D d{pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
+                                   pl.cols.src_step * A.LDim(), At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
+                                   pl.cols.dst_step * B.LDim()};
+                    exec::Copy2DBatch(dev, t, &d, 1, true, j.alpha, st);
                 }
-            } else if (rc[q] > 0) {
+            } else if (j.rc[q] > 0) {
                 auto d = unpack_desc(q);
-                exec::Copy2DBatch(dev, t, &d, 1, true, alpha, st);
+                exec::Copy2DBatch(dev, t, &d, 1, true, j.alpha, st);
             }
         }
     }
-    // sbuf/rbuf return to the pool stream-ordered on `st`
+    // sbuf/rbuf return to the pool stream-ordered on B's stream
+}
+
+Comm::VSet ExchangeOf(TransferJob& j) {
+    return Comm::VSet{j.A->Type(), j.sbuf.data(), &j.sc, &j.sd, j.rbuf.data(), &j.rc, &j.rd};
+}
+
+void Transfer(const DistMatrix& A, DistMatrix& B, bool contract, double alpha) {
+    TransferJob j{&A, &B, contract, alpha};
+    TransferPrepare(j);
+    if (j.cross) A.G().VC().AllToAllV(A.Type(), j.sbuf.data(), j.sc, j.sd, j.rbuf.data(), j.rc, j.rd, B.Dev(), B.Stream());
+    TransferFinish(j);
 }
 
 void LocalTransposeInto(const DistMatrix& A, DistMatrix& T) {
@@ -317,6 +349,37 @@ void Copy(const DistMatrix& A, DistMatrix& B) {
     PrepareTarget(A, B);
     if (B.Height() == 0 || B.Width() == 0) return;
     Transfer(A, B, false, 0.0);
+}
+
+void CopyGroup(const std::vector<std::pair<const DistMatrix*, DistMatrix*>>& pairs) {
+    // one shared exchange only when every pair is a same-type, same-device
+    // redistribution on one grid with its target on one stream
+    bool group = pairs.size() > 1;
+    for (const auto& pr : pairs) {
+        const DistMatrix& A = *pr.first;
+        DistMatrix& B = *pr.second;
+        group = group && A.Type() == B.Type() && A.Dev() == B.Dev() && &A.G() == &pairs[0].first->G() &&
+                &B.G() == &A.G() && B.Stream() == pairs[0].second->Stream();
+    }
+    if (!group) {
+        for (const auto& pr : pairs) Copy(*pr.first, *pr.second);
+        return;
+    }
+    ELX_TRACE("El::Copy (grouped redistributions)");
+    std::vector<TransferJob> jobs;
+    jobs.reserve(pairs.size());
+    for (const auto& pr : pairs) {
+        CheckCompatible(*pr.first, *pr.second);
+        PrepareTarget(*pr.first, *pr.second);
+        if (pr.second->Height() == 0 || pr.second->Width() == 0) continue;
+        jobs.push_back(TransferJob{pr.first, pr.second, false, 0.0});
+    }
+    for (auto& j : jobs) TransferPrepare(j);
+    std::vector<Comm::VSet> sets;
+    for (auto& j : jobs)
+        if (j.cross) sets.push_back(ExchangeOf(j));
+    if (!sets.empty()) jobs[0].A->G().VC().AllToAllVGroup(sets, jobs[0].B->Dev(), jobs[0].B->Stream());
+    for (auto& j : jobs) TransferFinish(j);
 }
 
 void Transpose(const DistMatrix& A, DistMatrix& B) {

@@ -1,11 +1,16 @@
 // The DistMatrix redistribution engine and the distributed BLAS-1 front doors.
 #pragma once
+#include <utility>
+#include <vector>
 #include "distmatrix.hpp"
 
 namespace elx {
 
 // B := A (DistMatrix::operator=), any element-wise pair, any alignments.
 void Copy(const DistMatrix& A, DistMatrix& B);
+// Several Copy(A_i, B_i) whose exchanges share one grouped all-to-all (targets
+// on one stream, same type and device on one grid; otherwise plain Copy each)
+void CopyGroup(const std::vector<std::pair<const DistMatrix*, DistMatrix*>>& pairs);
 // B := A^T (El::Transpose on DistMatrices; ADJOINT == TRANSPOSE for real types)
 void Transpose(const DistMatrix& A, DistMatrix& B);
 // B += alpha * (sum of A's redundant partial copies), redistributed to B (AxpyContract)
