@@ -1,3 +1,4 @@
+#include <cstdlib>
 #include "exec.hpp"
 #include "../kernels/elem.hpp"
 #include <cmath>
@@ -106,10 +107,21 @@ void check(hipError_t e, const char* what) {
 
 }  // namespace
 
+// Pack / unpack launches on the comm stream run beside full-machine MFMA
+// updates, so they are capped at ELX_COMM_COPY_WGS workgroups (default 256, one
+// per CU): uncapped launches of thousands of workgroups at the comm stream's
+// priority slowed the MFMA updates by 5-10 %, caps of 256-512 by 0-2 %
+// (profiles/r02_comm_copy_cap.log; 0 = uncapped)
+int CommCopyWGs() {
+    static const int v = [] { const char* e = getenv("ELX_COMM_COPY_WGS"); return e ? atoi(e) : 256; }();
+    return v;
+}
+
 void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s) {
     if (nd <= 0) return;
     if (dev == Device::GPU) {
-        check(kern::copy2d_batch(static_cast<int>(t), d, nd, axpy, alpha, s), "copy2d_batch");
+        const int cap = s != nullptr && s == Runtime::Get().CommStream() ? CommCopyWGs() : 0;
+        check(kern::copy2d_batch(static_cast<int>(t), d, nd, axpy, alpha, s, cap), "copy2d_batch");
         return;
     }
     for (int q = 0; q < nd; ++q) HOST_DTYPE_SWITCH(t, S, cpu_copy<S>(d[q], axpy, alpha));

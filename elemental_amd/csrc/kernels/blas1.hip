@@ -589,7 +589,7 @@ bool TransposeViaLds() {
 
 }  // namespace
 
-hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s) {
+hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s, int max_wgs) {
     for (int base = 0; base < nd; base += kMaxCopyBatch) {
         CopyBatch b{};
         const int cnt = (nd - base) < kMaxCopyBatch ? (nd - base) : kMaxCopyBatch;
@@ -617,25 +617,27 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
             if (wt > maxwt) maxwt = wt;
         }
         if (used == 0) continue;
+        // workgroups per descriptor row of the grid under the caller's cap
+        const i64 cap = max_wgs > 0 ? std::max<i64>(1, max_wgs / used) : (i64)1 << 30;
         // 16-bit: register blocks (4.08 vs 3.59 TB/s at 16384 x 8192); f32 / f64
         // keep the LDS tile, which measured faster for them (4.71 vs 4.19, 5.04
         // vs 4.93 TB/s; profiles/r02_transpose_ab.log)
         if (!cols && tvec_all && es == 2 && !TransposeViaLds()) {
             // ~8 workgroups per CU: 32 waves per CU over the batch's wave tiles
-            const unsigned gx = (unsigned)std::max<i64>(1, std::min<i64>((maxwt + 3) / 4, 2048));
+            const unsigned gx = (unsigned)std::max<i64>(1, std::min<i64>(std::min<i64>((maxwt + 3) / 4, 2048), cap));
             dim3 grid(gx, used);
             ELX_DTYPE_SWITCH(dtype, T,
                 if (axpy) hipLaunchKernelGGL((transpose_vec_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
                 else hipLaunchKernelGGL((transpose_vec_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
         } else if (cols) {
             // ~16 workgroups per CU across the batch
-            const i64 gx = std::max<i64>(1, std::min<i64>((maxvec + NT * UNROLL - 1) / (NT * UNROLL), 1 << 20));
+            const i64 gx = std::max<i64>(1, std::min<i64>(std::min<i64>((maxvec + NT * UNROLL - 1) / (NT * UNROLL), 1 << 20), cap));
             dim3 grid((unsigned)gx, used);
             ELX_DTYPE_SWITCH(dtype, T,
                 if (axpy) hipLaunchKernelGGL((copy_cols_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);
                 else hipLaunchKernelGGL((copy_cols_kernel<T, false>), grid, dim3(NT), 0, s, b, alpha));
         } else {
-            const unsigned gx = (unsigned)(maxtiles > 4096 ? 4096 : maxtiles);
+            const unsigned gx = (unsigned)std::max<i64>(1, std::min<i64>(maxtiles > 4096 ? 4096 : maxtiles, cap));
             dim3 grid(gx, used);
             ELX_DTYPE_SWITCH(dtype, T,
                 if (axpy) hipLaunchKernelGGL((copy2d_kernel<T, true>), grid, dim3(NT), 0, s, b, alpha);

@@ -80,7 +80,8 @@ struct Copy2D {
 constexpr int kMaxCopyBatch = 16;
 // Executes up to any number of descriptors (chunks of kMaxCopyBatch per launch).
 // axpy=false: plain copy (bit-exact, alpha ignored); axpy=true: dst += alpha*src.
-hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
+// max_wgs > 0 caps the workgroups of the launch (grid-stride loops cover the rest)
+hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s, int max_wgs = 0);
 
 // Type-converting strided copy: dst(i,j) = (dst type) src(i,j), one rounding (elem.hpp).
 hipError_t convert2d(int src_dtype, int dst_dtype, const Copy2D& d, hipStream_t s);
