@@ -65,7 +65,9 @@ void Runtime::EnsureGPU() {
     ELX_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     // communication gets the higher priority so panel broadcasts are not
     // starved by the long-running MFMA update they overlap with
-    ELX_CHECK_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, hi));
+    // (ELX_COMM_PRIORITY=0: the compute stream's priority instead; A/B timing)
+    const char* pe = getenv("ELX_COMM_PRIORITY");
+    ELX_CHECK_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, pe && atoi(pe) == 0 ? lo : hi));
     ELX_CHECK_HIP(hipDeviceGetDefaultMemPool(&pool_, device_));
     uint64_t thresh = std::numeric_limits<uint64_t>::max();  // keep freed blocks cached
     ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolAttrReleaseThreshold, &thresh));
