@@ -288,13 +288,20 @@ int TeamCount(const DistMatrix& C, Int panels) {
 Int EffectivePanel(const Grid& g, Int K, DType t) {
     const Int nb = std::max<Int>(1, g_blocksize);
     Int kc = g_compute_panel;
-    // automatic: K/8, never below 2048, never above 8192.  C's HBM round trip
-    // per panel (16 B/element at fp64) against the panel's 2*kc FLOP/element:
-    // C3 on one GPU (K = 65536) runs 72.9 TF at kc = 8192 vs 71.9 at 4096
-    // (profiles/r02_trsm_kc.log); the deeper first panel exposes ~4 ms more of
-    // transfer at 8 GPUs, against ~1 % of a ~1 s step.  16-bit MFMAs are 32x
-    // faster per element for 1/4 of the C bytes: K/8 is their floor as well.
-    if (kc <= 0) kc = (g.Size() == 1) ? K : std::min<Int>(8192, std::max<Int>(2048, K / 8));
+    // automatic: C's HBM round trip per panel (read + write, 2s bytes per
+    // element) against the panel's 2*kc FLOP per element.
+    //  f64 / f32: K/8 in [2048, 8192]: C3 on one GPU (K = 65536) runs 72.9 TF at
+    //    kc = 8192 vs 71.9 at 4096 (profiles/r02_trsm_kc.log); the deeper first
+    //    panel's gather is cut to a quarter by SummaC's ramp.
+    //  f16 / bf16: the MFMAs are 16-32x faster per element for only 4x fewer C
+    //    bytes, so the round trip weighs ~8x more: K/2 in [2048, 16384]. C5's
+    //    local panel on 2x4 (16384 x 8192 x kc bf16) runs 1058 / 1256 / 1390 /
+    //    1458 TF at kc = 4096 / 8192 / 16384 / 32768 (profiles/r02_panel_depth.log).
+    const bool h16 = t == DType::F16 || t == DType::BF16;
+    if (kc <= 0)
+        kc = (g.Size() == 1) ? K
+             : h16          ? std::min<Int>(16384, std::max<Int>(2048, K / 2))
+                            : std::min<Int>(8192, std::max<Int>(2048, K / 8));
     kc = std::max<Int>(nb, (kc + nb - 1) / nb * nb);  // whole communication panels
     return std::max<Int>(1, kc);
 }
