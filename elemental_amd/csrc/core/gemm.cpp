@@ -294,14 +294,15 @@ Int EffectivePanel(const Grid& g, Int K, DType t) {
     //    kc = 8192 vs 71.9 at 4096 (profiles/r02_trsm_kc.log); the deeper first
     //    panel's gather is cut to a quarter by SummaC's ramp.
     //  f16 / bf16: the MFMAs are 16-32x faster per element for only 4x fewer C
-    //    bytes, so the round trip weighs ~8x more: K/2 in [2048, 16384]. C5's
+    //    bytes, so the round trip weighs ~8x more: K/4 in [2048, 8192]. C5's
     //    local panel on 2x4 (16384 x 8192 x kc bf16) runs 1058 / 1256 / 1390 /
-    //    1458 TF at kc = 4096 / 8192 / 16384 / 32768 (profiles/r02_panel_depth.log).
+    //    1458 TF at kc = 4096 / 8192 / 16384 / 32768 (profiles/r02_panel_depth.log);
+    //    past 8192 the gather of the panel after the (quarter-depth) first one
+    //    outgrows the first panel's update (each panel moves 8192*kc B per link
+    //    at 2x4), which costs more than the deeper update gains at ~50 GB/s/link.
     const bool h16 = t == DType::F16 || t == DType::BF16;
     if (kc <= 0)
-        kc = (g.Size() == 1) ? K
-             : h16          ? std::min<Int>(16384, std::max<Int>(2048, K / 2))
-                            : std::min<Int>(8192, std::max<Int>(2048, K / 8));
+        kc = (g.Size() == 1) ? K : std::min<Int>(8192, std::max<Int>(2048, h16 ? K / 4 : K / 8));
     kc = std::max<Int>(nb, (kc + nb - 1) / nb * nb);  // whole communication panels
     return std::max<Int>(1, kc);
 }
