@@ -480,15 +480,24 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
             ELX_CHECK_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         }
     }
-    // Panel p covers [kbeg(p), kbeg(p+1)).  On grids larger than 1x1 the first
-    // panel is a quarter of kc (whole communication panels): its gather is the
-    // one transfer no update hides, and the full-depth gather of panel 1 then
-    // runs behind panel 0's update (at 2x4, C3: ~30 ms of MFMA work against
-    // ~20 ms of transfer).  A 1x1 grid uses its panels in place: no ramp.
+    // Panel p covers [kb[p], kb[p+1]).  On grids larger than 1x1 the panels ramp
+    // up kc/4, kc/2, kc, kc, ... (whole communication panels): the first gather
+    // is the one transfer no update hides, and each later gather runs behind
+    // the previous panel's update, which the doubling keeps long enough for it
+    // (a single quarter-depth step left the second, full-depth gather exposed
+    // where a panel's transfer and update take similar time: 16-bit C5 at 2x4).
+    // A 1x1 grid uses its panels in place: no ramp.
     const Int nb = std::max<Int>(1, g_blocksize);
-    const Int kfirst = (g.Size() > 1 && kc >= 4 * nb && K > kc) ? std::max<Int>(nb, kc / 4 / nb * nb) : kc;
-    const int np = K == 0 ? 0 : K <= kfirst ? 1 : static_cast<int>(1 + (K - kfirst + kc - 1) / kc);
-    auto kbeg = [&](int p) { return p == 0 ? Int(0) : std::min<Int>(K, kfirst + Int(p - 1) * kc); };
+    std::vector<Int> kb{0};
+    if (g.Size() > 1 && kc >= 4 * nb && K > kc) {
+        for (Int d : {kc / 4, kc / 2}) {
+            d = std::max<Int>(nb, d / nb * nb);
+            if (kb.back() < K) kb.push_back(std::min<Int>(K, kb.back() + d));
+        }
+    }
+    while (kb.back() < K) kb.push_back(std::min<Int>(K, kb.back() + kc));
+    const int np = static_cast<int>(kb.size()) - 1;
+    auto kbeg = [&](int p) { return kb[static_cast<size_t>(p)]; };
     const int call_id = Prof().calls++;
     Buffer trrk_tmp;
 

@@ -72,9 +72,10 @@ def test_gemm_multi_panel_pipeline(world, height):
 
 @pytest.mark.parametrize("world,height", [(2, 1), (8, 2)])
 def test_gemm_first_panel_ramp(world, height):
-    """Compute panel 16 = 4 x nb on a grid larger than 1x1: the first panel is a
-    quarter deep (4 columns), then 16-column panels and a ragged last one (k = 61:
-    4, 16, 16, 16, 9); k = 13 < kc and k = 20 (4 + 16) bound the panel count."""
+    """Compute panel 16 = 4 x nb on a grid larger than 1x1: the panels ramp up a
+    quarter and a half deep, then 16 columns, and a ragged last one (k = 61:
+    4, 8, 16, 16, 16, 1); k = 13 < kc (4, 8, 1) and k = 20 (4, 8, 8) end inside
+    the ramp."""
     _spawn(W.gemm_worker, world, height, el.CPU, el.F64, [(21, 18, 61), (9, 11, 13), (10, 7, 20)],
            [el.GEMM_SUMMA_C], 4, 47, 16)
 

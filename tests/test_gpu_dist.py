@@ -90,8 +90,8 @@ def test_gpu_summa_multi_panel_distributed(world, height):
 
 @pytest.mark.parametrize("world,height", [(2, 1), (8, 2)])
 def test_gpu_summa_first_panel_ramp(world, height):
-    """Compute panel 64 = 4 x nb on a grid larger than 1x1: a 16-column first panel,
-    then 64-column panels (k = 130: 16, 64, 50; k = 80: 16, 64)."""
+    """Compute panel 64 = 4 x nb on a grid larger than 1x1: the panels ramp up
+    16, 32, then 64 columns (k = 130: 16, 32, 64, 18; k = 80: 16, 32, 32)."""
     _spawn(W.gemm_worker, world, height, el.GPU, el.F64, [(45, 37, 130), (33, 20, 80)], [el.GEMM_SUMMA_C], 16, 53,
            64)
 
