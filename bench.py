@@ -47,6 +47,23 @@ KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_f32g_kernel (LDS-DMA
           "bf16": "gemm_h4d_kernel<bf16>", "f16": "gemm_h4d_kernel<f16>"}
 
 
+_WATCHDOG = None  # elemental_amd.el once imported
+
+
+def stage(name: str, seconds: float):
+    """Progress line on stderr and a watchdog deadline for the next stage: past
+    it (or on an asynchronous RCCL error) the library aborts its RCCL
+    communicators and the process exits naming the stage (elx_watchdog_stage),
+    instead of hanging a multi-GPU run."""
+    if _WATCHDOG is None:
+        return
+    if os.environ.get("ELX_BENCH_HANG") == name:
+        # fault injection for tests/test_gpu_dist.py: this stage hangs
+        _WATCHDOG.watchdog_stage(name, 2.0)
+        time.sleep(120)
+    _WATCHDOG.watchdog_stage(name, seconds)
+
+
 def cpu_baseline(seconds_target: float = 10.0) -> dict:
     """The CPU leg (BASELINE.md §3): C1 (BASELINE.json configs[0]), El::Gemm NN
     fp64 4096^3 on a 2x2 grid, run as the reference's CPU path runs it: SUMMA_NNC
@@ -132,6 +149,58 @@ def associativity_residual(el, grid, n: int = 4096, nrhs: int = 100) -> float:
     return float(np.linalg.norm(out[0]) / np.linalg.norm(out[1]))
 
 
+# unit roundoff of each storage type
+UNIT_ROUNDOFF = {"f64": 2.0 ** -53, "f32": 2.0 ** -24, "bf16": 2.0 ** -8, "f16": 2.0 ** -11}
+
+
+def check_tolerance(dtype: str, k: int) -> tuple[float, str]:
+    """Bound for the associativity residual of a full-size point: 10 u sqrt(k)
+    for f64 / f32 (the probabilistic normwise bound of a length-k sum), 16 u for
+    f16 / bf16 (f32 accumulation: the storage roundings of Z, Y and C_f
+    dominate, a few u)."""
+    u = UNIT_ROUNDOFF[dtype]
+    if dtype in ("f64", "f32"):
+        return 10.0 * u * k ** 0.5, "10 u sqrt(k)"
+    return 16.0 * u, "16 u (f32 accumulation)"
+
+
+def verify_point(el, grid, DT, dtype: str, oA, step, A, B, C, k: int, alpha: float = 0.5, beta: float = -0.5,
+                 nrhs: int = 100) -> dict:
+    """The reference's associativity check on a timed configuration itself
+    (tests/blas_like/Gemm_Suite.cpp:91-132,190-195; tests/blas_like/Gemm.cpp:15-49):
+    C0 := C, one more step() through the very path that was timed (C_f = alpha
+    op(A) B + beta C0), then Y = alpha op(A) (B X) + beta C0 X and
+    ||Y - C_f X||_F / ||Y||_F with X Uniform-like in [-0.25, 0.25), n x 100,
+    every product an El::Gemm on the same grid.  No oracle: self-consistency at
+    BASELINE sizes, as the reference checks its own runs."""
+    m, n = C.Height(), C.Width()
+    C0 = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU)
+    C0.assign(C)
+    step()
+    X = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=n, width=nrhs).fill_hash(11, 0.0, 0.25)
+    Z = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=nrhs)
+    Y = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=nrhs)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, B, X, 0.0, Z)          # Z = B X
+    el.Gemm(oA, el.NORMAL, alpha, A, Z, 0.0, Y)               # Y = alpha op(A) Z
+    el.Gemm(el.NORMAL, el.NORMAL, beta, C0, X, 1.0, Y)        # Y += beta C0 X
+    ynorm = el.FrobeniusNorm(Y)
+    el.Gemm(el.NORMAL, el.NORMAL, -1.0, C, X, 1.0, Y)         # E = Y - C_f X
+    enorm = el.FrobeniusNorm(Y)
+    del C0, X, Z, Y
+    r = enorm / ynorm if ynorm > 0 else float("inf")
+    tol, rule = check_tolerance(dtype, k)
+    return {"check": f"associativity ||Y - C_f X||_F/||Y||_F, {nrhs} rhs, at this point's full size "
+                     "(tests/blas_like/Gemm.cpp:15-49)",
+            "residual": r, "tol": tol, "tol_rule": rule, "ok": bool(r <= tol)}
+
+
+def est_seconds(flops: float, dtype: str, world: int) -> float:
+    """Pessimistic duration of `flops` on `world` GPUs (half the measured rates),
+    for the watchdog deadlines."""
+    rate = {"f64": 35e12, "f32": 70e12, "bf16": 600e12, "f16": 600e12}[dtype] * world
+    return flops / rate
+
+
 def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n: int = 65536,
                kc: int = 8192) -> dict:
     """C3 (El::Gemm NN fp64 m=n=k=65536) on a 1x1 grid through the panel path:
@@ -139,6 +208,7 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
     panels are gathered; here they are views), so value_N / (N * value) is a
     same-problem strong-scaling efficiency."""
     el.SetComputePanel(kc)
+    stage("c3_1gpu", 120 + 4 * (steps + warmup) * est_seconds(2.0 * n ** 3, "f64", 1))
     try:
         A = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(1, 0.0, 0.1)
         B = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(2, 0.0, 0.1)
@@ -155,6 +225,9 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
         elapsed = time.perf_counter() - t0
         prof = profile_summary(L, ctypes)
         L.call("elx_set_profiling", 0)
+        stage("c3_1gpu verify", 120 + 4 * est_seconds(2.0 * n ** 3, "f64", 1))
+        check = verify_point(el, grid, el.F64, "f64", el.NORMAL,
+                             lambda: el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C), A, B, C, n)
     finally:
         el.SetComputePanel(kc_restore)
     value = 2.0 * n ** 3 * steps / elapsed / 1e12
@@ -169,7 +242,8 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
             "roofline": {"bound": "mfma", "kernel": KERNEL["f64"], "achieved": round(ach, 3),
                          "peak": PEAK_TFLOPS["f64"], "frac": round(ach / PEAK_TFLOPS["f64"], 4),
                          "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)},
-            "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3)}
+            "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3),
+            "verify": check}
 
 
 def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: int, world: int, size: int = 0) -> dict:
@@ -194,6 +268,7 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
         B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
         workload = f"C5: El::Gemm NN bf16 m=n=k={m} on [MC,MR], Grid {gshape}"
     C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=n).fill_hash(3, 0.0, 0.1)
+    stage(config, 120 + 4 * (warmup + steps) * est_seconds(2.0 * m * n * k, dtype, world))
     for _ in range(warmup):
         el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
     barrier()
@@ -217,7 +292,11 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
                         "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)}}
     if world > 1:
         out["collectives"] = collectives_summary(prof, steps)
+    stage(f"{config} verify", 120 + 4 * est_seconds(2.0 * m * n * k, dtype, world))
+    out["verify"] = verify_point(el, grid, DT, dtype, oA, lambda: el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C),
+                                 A, B, C, k)
     if config == "c5":
+        stage("c5 entrywise", 120)
         loc = A.LocalHeight() * A.LocalWidth()
         ew = {}
         for name, fn in (("axpy", lambda: el.Axpy(0.5, A, C)), ("hadamard", lambda: el.Hadamard(A, B, C))):
@@ -259,6 +338,9 @@ def main():
     import torch
     from elemental_amd import el
     from elemental_amd import _lib as L
+    global _WATCHDOG
+    _WATCHDOG = el
+    stage("init", 600)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -322,19 +404,23 @@ def main():
     def step():
         return el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
 
+    step_flops = 2.0 * m * n * k
     residual = None
     if world > 1 and not args.no_residual:
         # correctness on this very grid before timing (no oracle): the reference's
         # associativity check through the distributed path
+        stage("residual", 300)
         try:
             residual = associativity_residual(el, grid)
         except Exception as e:  # report, never lose the timed line to the check
             residual = f"error: {e}"
         barrier()
 
+    stage("warmup", 120 + 4 * args.warmup * est_seconds(step_flops, dtype, world))
     for _ in range(args.warmup):
         step()
     barrier()
+    stage("timed", 120 + 4 * args.steps * est_seconds(step_flops, dtype, world))
     L.call("elx_set_profiling", 1)
     el.comm_stats_reset()
     barrier()
@@ -355,7 +441,7 @@ def main():
         return float(t.item())
 
     elapsed = max_over_ranks(elapsed)
-    total_flops = 2.0 * m * n * k * args.steps
+    total_flops = step_flops * args.steps
     value = total_flops / elapsed / 1e12
     avg_ms = prof["gemm_ms"] / max(prof["launches"], 1)
     flops_per_launch = prof["flops"] / max(prof["launches"], 1)
@@ -407,82 +493,124 @@ def main():
     cus = ctypes.c_int()
     L.call("elx_reserved_cus", ctypes.byref(cus))
     out["config"]["comm_reserved_cus"] = cus.value
+
+    # the timed point itself, checked at full size through the same path (one
+    # more, untimed step)
+    stage("verify", 120 + 4 * est_seconds(step_flops, dtype, world))
+    try:
+        out["verify"] = verify_point(el, grid, DT, dtype, oA, step, A, B, C, k)
+    except Exception as e:
+        out["verify"] = {"error": str(e), "ok": False}
+    barrier()
+
+    # from here on the line exists: if a later (optional) stage overruns, the
+    # watchdog prints it with that stage marked, and the process exits 0
+    def epitaph(pending: str | None):
+        if rank != 0:
+            el.watchdog_epitaph("", 0)
+            return
+        line = dict(out)
+        if pending:
+            line[pending] = {"error": f"watchdog: stage {pending} overran its deadline (RCCL aborted)"}
+        el.watchdog_epitaph(json.dumps(line), 0)
+
+    def extra(key: str, fn):
+        epitaph(key)
+        try:
+            out[key] = fn()
+        except Exception as e:  # evidence only: never lose the driver's line to it
+            out[key] = {"error": str(e)}
+        epitaph(None)
+
     if config == "c5":
         # DistMatrix Axpy / Hadamard on the [MC,MR] operands (no exchange: each
         # rank updates its local block); HBM bytes 3 x local elements x size
-        es = {"f64": 8, "f32": 4, "bf16": 2, "f16": 2}[dtype]
-        loc = A.LocalHeight() * A.LocalWidth()
-        ew = {}
-        for name, fn, reps in (("axpy", lambda: el.Axpy(0.5, A, C), 20), ("hadamard", lambda: el.Hadamard(A, B, C), 20)):
-            fn()
-            barrier()
-            t1 = time.perf_counter()
-            for _ in range(reps):
+        def entrywise():
+            stage("entrywise", 120)
+            es = {"f64": 8, "f32": 4, "bf16": 2, "f16": 2}[dtype]
+            loc = A.LocalHeight() * A.LocalWidth()
+            ew = {}
+            for name, fn, reps in (("axpy", lambda: el.Axpy(0.5, A, C), 20),
+                                   ("hadamard", lambda: el.Hadamard(A, B, C), 20)):
                 fn()
-            barrier()
-            dt = max_over_ranks((time.perf_counter() - t1) / reps)
-            gbs = 3 * es * loc / dt / 1e9
-            ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
-                        "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
-        out["entrywise"] = ew
+                barrier()
+                t1 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                barrier()
+                dt = max_over_ranks((time.perf_counter() - t1) / reps)
+                gbs = 3 * es * loc / dt / 1e9
+                ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
+                            "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+            return ew
+        extra("entrywise", entrywise)
     if config == "c4":
         # the same product with [MC,MR] inputs: SUMMA_DOT's read
         # proxies first redistribute A and B to [VC,*] (TN.hpp:384-391), inside
         # the timed region
-        del A, B
-        Am = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
-        Bm = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
-        el.Gemm(oA, el.NORMAL, 0.5, Am, Bm, -0.5, C)
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
+        def mcmr():
+            nonlocal A, B
+            A = B = None
+            stage("c4_mcmr_inputs", 120 + 4 * (args.steps + 1) * est_seconds(step_flops, dtype, world))
+            Am = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=m).fill_hash(1, 0.0, 0.1)
+            Bm = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
             el.Gemm(oA, el.NORMAL, 0.5, Am, Bm, -0.5, C)
-        barrier()
-        dt = max_over_ranks(time.perf_counter() - t1)
-        out["c4_mcmr_inputs"] = {"workload": workload.replace("[VC,STAR]", "[MC,MR] (proxied to [VC,STAR] each call)"),
-                                 "value": round(2.0 * m * n * k * args.steps / dt / 1e12, 3), "unit": "TFLOP/s",
-                                 "ms_per_step": round(dt / args.steps * 1e3, 3)}
-        del Am, Bm
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                el.Gemm(oA, el.NORMAL, 0.5, Am, Bm, -0.5, C)
+            barrier()
+            dt = max_over_ranks(time.perf_counter() - t1)
+            return {"workload": workload.replace("[VC,STAR]", "[MC,MR] (proxied to [VC,STAR] each call)"),
+                    "value": round(2.0 * m * n * k * args.steps / dt / 1e12, 3), "unit": "TFLOP/s",
+                    "ms_per_step": round(dt / args.steps * 1e3, 3)}
+        extra("c4_mcmr_inputs", mcmr)
     if world == 1 and config == "c2" and not args.n and not args.no_c3_1gpu:
         # the same problem as the driver's N>1 lines (C3, n = 65536, kc = 8192
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
         A = B = C = None  # release the C2 operands before the n = 65536 ones
-        out["c3_1gpu"] = c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc)
+        extra("c3_1gpu", lambda: c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc))
     if config in ("c2", "c3") and (not args.n or rehearse) and not args.no_extra_configs:
         # the other BASELINE configs, measured in the same run on the same grid
         # (N = 1: c4_1gpu / c5_1gpu; N > 1: c4 / c5 on Grid::DefaultHeight(N))
         A = B = C = None  # release the main operands (no-op when already released)
         for cfg, st in (("c4", 2), ("c5", 5)):
             key = f"{cfg}_1gpu" if world == 1 else cfg
-            try:
-                out[key] = config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1, world, args.n)
-            except Exception as e:  # evidence only: never lose the driver's line to it
-                out[key] = {"error": str(e)}
+            extra(key, lambda cfg=cfg, st=st: config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1, world,
+                                                            args.n))
     if world == 1 and config == "c2" and not args.n and not args.no_extra_configs:
         # C1's problem (NN f64 4096^3) on the GPU, beside the CPU leg's same problem
-        n1 = 4096
-        A1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(1, 0.0, 0.1)
-        B1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(2, 0.0, 0.1)
-        C1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(3, 0.0, 0.1)
-        for _ in range(3):
-            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(20):
-            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
-        barrier()
-        dt = (time.perf_counter() - t1) / 20
-        out["c1_1gpu"] = {"workload": "C1's problem on the GPU: El::Gemm NN f64 m=n=k=4096, Grid 1x1",
-                          "value": round(2.0 * n1 ** 3 / dt / 1e12, 3), "unit": "TFLOP/s", "steps": 20,
-                          "ms_per_step": round(dt * 1e3, 3)}
-        del A1, B1, C1
+        def c1():
+            stage("c1_1gpu", 120)
+            n1 = 4096
+            A1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(1, 0.0, 0.1)
+            B1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(2, 0.0, 0.1)
+            C1 = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n1, width=n1).fill_hash(3, 0.0, 0.1)
+            for _ in range(3):
+                el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(20):
+                el.Gemm(el.NORMAL, el.NORMAL, 0.5, A1, B1, -0.5, C1)
+            barrier()
+            dt = (time.perf_counter() - t1) / 20
+            return {"workload": "C1's problem on the GPU: El::Gemm NN f64 m=n=k=4096, Grid 1x1",
+                    "value": round(2.0 * n1 ** 3 / dt / 1e12, 3), "unit": "TFLOP/s", "steps": 20,
+                    "ms_per_step": round(dt * 1e3, 3)}
+        extra("c1_1gpu", c1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline()
+        def cpu():
+            stage("cpu_baseline", 300)
+            return cpu_baseline()
+        extra("cpu_baseline", cpu)
+    stage("report", 300)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    el.watchdog_epitaph("", 0)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    stage("done", 0)
 
 
 if __name__ == "__main__":

@@ -50,6 +50,12 @@ _SIGS = {
     "elx_stream_create": (_i, [POINTER(c_void_p)]),
     "elx_stream_destroy": (_i, [_vp]),
     "elx_stream_synchronize": (_i, [_vp]),
+    "elx_default_event": (_i, [POINTER(c_void_p)]),
+    "elx_event_create": (_i, [POINTER(c_void_p)]),
+    "elx_event_destroy": (_i, [_vp]),
+    "elx_event_record": (_i, [_vp, _vp]),
+    "elx_stream_wait_event": (_i, [_vp, _vp]),
+    "elx_event_synchronize": (_i, [_vp]),
     "elx_pool_alloc": (_i, [POINTER(c_void_p), c_size_t, _vp]),
     "elx_pool_free": (_i, [_vp, _vp]),
     "elx_pool_trim": (_i, [c_size_t]),
@@ -90,6 +96,11 @@ _SIGS = {
     "elx_comm_rank": (_i, [_vp, POINTER(c_int)]),
     "elx_comm_size": (_i, [_vp, POINTER(c_int)]),
     "elx_comm_destroy": (_i, [_vp]),
+    "elx_comm_world": (_i, [POINTER(c_void_p)]),
+    "elx_comm_set_world": (_i, [_vp]),
+    "elx_rendezvous_bcast": (_i, [_vp, c_size_t, _i, _i, c_char_p, _i, _d]),
+    "elx_watchdog_stage": (_i, [c_char_p, _d]),
+    "elx_watchdog_epitaph": (_i, [c_char_p, _i]),
     "elx_comm_allgather": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
     "elx_comm_reduce_scatter": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
     "elx_comm_barrier": (_i, [_vp]),
@@ -148,6 +159,11 @@ _SIGS = {
     "elx_dm_scale_trapezoid": (_i, [_d, _i, _vp, _i64]),
     "elx_set_blocksize": (_i, [_i64]),
     "elx_blocksize": (_i64, []),
+    "elx_push_blocksize": (_i, [_i64]),
+    "elx_pop_blocksize": (_i, []),
+    "elx_empty_blocksize_stack": (_i, []),
+    "elx_initialize": (_i, []),
+    "elx_finalize": (_i, []),
     "elx_set_compute_panel": (_i, [_i64]),
     "elx_last_gemm_algorithm": (_i, []),
     "elx_set_stream_pool_size": (_i, [_i]),

@@ -35,6 +35,11 @@ void CheckOp(int o) {
     if (o != ELX_NORMAL && o != ELX_TRANSPOSE && o != ELX_ADJOINT) throw LogicError(Cat("invalid orientation ", o));
 }
 hipStream_t S(void* s) { return Runtime::Get().Resolve(s); }
+// the handle elx_comm_world lends out (never freed)
+elx_comm_s& WorldHandle() {
+    static elx_comm_s* h = new elx_comm_s{};
+    return *h;
+}
 }  // namespace
 
 void SetLastError(const std::string& msg) { g_last_error = msg; }
@@ -72,6 +77,44 @@ int elx_stream_create(void** stream) {
 }
 int elx_stream_destroy(void* stream) { return Guard([&] { ELX_CHECK_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream))); }); }
 int elx_stream_synchronize(void* stream) { return Guard([&] { ELX_CHECK_HIP(hipStreamSynchronize(S(stream))); }); }
+int elx_default_event(void** event) {
+    return Guard([&] {
+        Runtime::Get().EnsureGPU();
+        static hipEvent_t ev = [] {
+            hipEvent_t e;
+            ELX_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            return e;
+        }();
+        *event = ev;
+    });
+}
+int elx_event_create(void** event) {
+    return Guard([&] {
+        Runtime::Get().EnsureGPU();
+        hipEvent_t e;
+        ELX_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        *event = e;
+    });
+}
+int elx_event_destroy(void* event) { return Guard([&] { ELX_CHECK_HIP(hipEventDestroy(static_cast<hipEvent_t>(event))); }); }
+int elx_event_record(void* event, void* stream) {
+    return Guard([&] {
+        ELX_REQUIRE(event, "null event");
+        ELX_CHECK_HIP(hipEventRecord(static_cast<hipEvent_t>(event), S(stream)));
+    });
+}
+int elx_stream_wait_event(void* stream, void* event) {
+    return Guard([&] {
+        ELX_REQUIRE(event, "null event");
+        ELX_CHECK_HIP(hipStreamWaitEvent(S(stream), static_cast<hipEvent_t>(event), 0));
+    });
+}
+int elx_event_synchronize(void* event) {
+    return Guard([&] {
+        ELX_REQUIRE(event, "null event");
+        ELX_CHECK_HIP(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+    });
+}
 
 int elx_pool_alloc(void** ptr, size_t bytes, void* stream) {
     return Guard([&] { *ptr = Runtime::Get().Alloc(bytes, S(stream)); });
@@ -392,6 +435,24 @@ int elx_comm_wrap_rccl(elx_comm_t* comm, void* nccl_comm) {
 int elx_comm_rank(elx_comm_t c, int* rank) { return Guard([&] { *rank = c->c->Rank(); }); }
 int elx_comm_size(elx_comm_t c, int* size) { return Guard([&] { *size = c->c->Size(); }); }
 int elx_comm_destroy(elx_comm_t c) { return Guard([&] { delete c; }); }
+int elx_comm_world(elx_comm_t* comm) {
+    return Guard([&] {
+        WorldHandle().c = WorldComm();
+        *comm = &WorldHandle();
+    });
+}
+int elx_comm_set_world(elx_comm_t comm) {
+    return Guard([&] {
+        ELX_REQUIRE(comm && comm->c, "null comm");
+        WorldComm() = comm->c;
+        WorldHandle().c = comm->c;
+    });
+}
+int elx_rendezvous_bcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s) {
+    return Guard([&] { RendezvousBcast(data, bytes, rank, size, addr, port, timeout_s); });
+}
+int elx_watchdog_stage(const char* name, double seconds) { return Guard([&] { WatchdogStage(name, seconds); }); }
+int elx_watchdog_epitaph(const char* text, int exit_code) { return Guard([&] { WatchdogEpitaph(text, exit_code); }); }
 int elx_comm_allgather(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
     return Guard([&] {
         const Device d = c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU;
@@ -595,7 +656,29 @@ int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset) {
     return Guard([&] { ScaleTrapezoid(alpha, uplo, M(A), offset); });
 }
 int elx_set_blocksize(int64_t nb) { return Guard([&] { SetBlocksize(nb); }); }
-int64_t elx_blocksize(void) { return Blocksize(); }
+int64_t elx_blocksize(void) {
+    int64_t nb = -1;
+    (void)Guard([&] { nb = Blocksize(); });
+    return nb;
+}
+int elx_push_blocksize(int64_t nb) { return Guard([&] { PushBlocksizeStack(nb); }); }
+int elx_pop_blocksize(void) { return Guard([&] { PopBlocksizeStack(); }); }
+int elx_empty_blocksize_stack(void) { return Guard([&] { EmptyBlocksizeStack(); }); }
+int elx_initialize(void) {
+    return Guard([&] {
+        InitWorldFromEnv();
+        EmptyBlocksizeStack();
+        PushBlocksizeStack(128);
+        InitializeRandom(true, WorldComm()->Rank());
+    });
+}
+int elx_finalize(void) {
+    return Guard([&] {
+        WorldComm() = Comm::Self();
+        if (WorldHandle().c) WorldHandle().c = WorldComm();
+        EmptyBlocksizeStack();
+    });
+}
 int elx_set_compute_panel(int64_t kc) { return Guard([&] { SetComputePanel(kc); }); }
 int elx_last_gemm_algorithm(void) { return LastGemmAlgorithm(); }
 int elx_set_stream_pool_size(int n) { return Guard([&] { SetStreamPoolSize(n); }); }

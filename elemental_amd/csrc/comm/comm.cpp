@@ -1,7 +1,19 @@
 #include "comm.hpp"
-#include <chrono>
-#include <cstring>
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
 
 namespace elx {
 
@@ -54,6 +66,69 @@ void CommProfiler::Stats(double& ms, int64_t& bytes, int64_t& calls) {
 
 namespace {
 
+double Now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Watchdog {
+    std::mutex mu;
+    std::string stage = "init";
+    double deadline = 0;  // steady-clock seconds; 0 = no deadline
+    double budget = 0;
+    std::vector<ncclComm_t> comms;
+    bool started = false;
+    std::string epitaph;  // written to stdout before exiting (e.g. a result line already measured)
+    int epitaph_code = kWatchdogExit;
+
+    [[noreturn]] void Fail(const std::string& why) {
+        const int code = epitaph_code;
+        std::fprintf(stderr, "[elx watchdog] FATAL in stage '%s': %s; aborting %zu RCCL communicator(s), exit %d\n",
+                     stage.c_str(), why.c_str(), comms.size(), code);
+        std::fflush(stderr);
+        for (ncclComm_t c : comms) (void)ncclCommAbort(c);
+        if (!epitaph.empty()) std::fprintf(stdout, "%s\n", epitaph.c_str());
+        std::fflush(stdout);
+        _exit(code);
+    }
+    void Loop() {
+        for (;;) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(50));
+            std::lock_guard<std::mutex> lk(mu);
+            for (ncclComm_t c : comms) {
+                ncclResult_t e = ncclSuccess;
+                if (ncclCommGetAsyncError(c, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress)
+                    Fail(Cat("RCCL asynchronous error: ", ncclGetErrorString(e)));
+            }
+            if (deadline > 0 && Now() > deadline) Fail(Cat("deadline of ", budget, " s exceeded"));
+        }
+    }
+};
+Watchdog& WD() {
+    static Watchdog* w = new Watchdog();  // never destroyed: the thread may outlive static teardown
+    return *w;
+}
+
+// Blocking communicators by default; ELX_RCCL_NONBLOCKING=1 creates them with
+// ncclConfig_t.blocking = 0 (every init, split and group end that returns
+// ncclInProgress is then polled by CheckNccl).  Either way a peer that never
+// arrives is caught by the watchdog's stage deadline (ncclCommAbort from the
+// watchdog thread, then exit), not by waiting forever.  Not the default: on
+// RCCL 2.26.6 (torch's librccl) a nonblocking world's ncclCommSplit handed back
+// a child that ncclCommUserRank rejected (invalid argument) at world size 1
+// (profiles/r03b_gputests_summary.log).
+bool NonBlocking() {
+    static const bool nb = [] {
+        const char* e = std::getenv("ELX_RCCL_NONBLOCKING");
+        return e && std::atoi(e) != 0;
+    }();
+    return nb;
+}
+ncclConfig_t CommConfig() {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = NonBlocking() ? 0 : 1;
+    return cfg;
+}
+
 ncclDataType_t NcclType(DType t) {
     switch (t) {
     case DType::F32: return ncclFloat32;
@@ -66,6 +141,14 @@ ncclDataType_t NcclType(DType t) {
 
 void CheckNccl(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw CommError(Cat("RCCL ", what, " failed: ", ncclGetErrorString(r)));
+}
+// result of a call on a (possibly nonblocking) communicator: wait out ncclInProgress
+void CheckNccl(ncclResult_t r, const char* what, ncclComm_t c) {
+    while (r == ncclInProgress) {
+        std::this_thread::yield();
+        if (ncclCommGetAsyncError(c, &r) != ncclSuccess) break;
+    }
+    CheckNccl(r, what);
 }
 
 void CopyBytes(Device dev, void* dst, const void* src, size_t bytes, hipStream_t s) {
@@ -105,7 +188,13 @@ std::shared_ptr<Comm> Comm::InitRCCL(int rank, int size, const unsigned char id[
     c->kind_ = Kind::RCCL;
     c->rank_ = rank;
     c->size_ = size;
-    CheckNccl(ncclCommInitRank(&c->nccl_, size, uid, rank), "ncclCommInitRank");
+    ncclConfig_t cfg = CommConfig();
+    ncclComm_t nc = nullptr;
+    const ncclResult_t r = ncclCommInitRankConfig(&nc, size, uid, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) CheckNccl(r, "ncclCommInitRankConfig");
+    c->nccl_ = nc;
+    WatchdogRegister(nc);
+    CheckNccl(r, "ncclCommInitRankConfig", nc);
     return c;
 }
 
@@ -136,7 +225,12 @@ std::shared_ptr<Comm> Comm::InitHost(int rank, int size, elx_host_coll_fn coll, 
 }
 
 Comm::~Comm() {
-    if (nccl_ && owned_) (void)ncclCommDestroy(nccl_);
+    if (nccl_ && owned_) {
+        WatchdogUnregister(nccl_);
+        ncclResult_t r = ncclCommFinalize(nccl_);
+        while (r == ncclInProgress && ncclCommGetAsyncError(nccl_, &r) == ncclSuccess) std::this_thread::yield();
+        (void)ncclCommDestroy(nccl_);
+    }
 }
 
 std::shared_ptr<Comm> Comm::Split(int color, int key) {
@@ -144,7 +238,15 @@ std::shared_ptr<Comm> Comm::Split(int color, int key) {
     auto c = std::shared_ptr<Comm>(new Comm());
     c->kind_ = kind_;
     if (kind_ == Kind::RCCL) {
-        CheckNccl(ncclCommSplit(nccl_, color, key, &c->nccl_, nullptr), "ncclCommSplit");
+        ncclConfig_t cfg = CommConfig();
+        const ncclResult_t r = ncclCommSplit(nccl_, color, key, &c->nccl_, &cfg);
+        if (r != ncclSuccess && r != ncclInProgress) CheckNccl(r, "ncclCommSplit");
+        CheckNccl(r, "ncclCommSplit", nccl_);
+        if (c->nccl_) {
+            WatchdogRegister(c->nccl_);
+            ncclResult_t st = ncclInProgress;
+            CheckNccl(st, "ncclCommSplit (child)", c->nccl_);
+        }
         CheckNccl(ncclCommUserRank(c->nccl_, &c->rank_), "ncclCommUserRank");
         CheckNccl(ncclCommCount(c->nccl_, &c->size_), "ncclCommCount");
         return c;
@@ -178,7 +280,7 @@ void Comm::AllGather(DType t, const void* send, void* recv, Int count, Device de
     if (count == 0) return;
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclAllGather(send, recv, count, NcclType(t), nccl_, s), "ncclAllGather");
+        CheckNccl(ncclAllGather(send, recv, count, NcclType(t), nccl_, s), "ncclAllGather", nccl_);
         return;
     }
     if (dev == Device::CPU) { HostCall(ELX_COLL_ALLGATHER, t, send, recv, count, 0, 0); return; }
@@ -200,7 +302,7 @@ void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Devic
     if (count == 0) return;
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclReduceScatter");
+        CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclReduceScatter", nccl_);
         return;
     }
     if (t == DType::F16 || t == DType::BF16) { HostSum16(true, t, send, recv, count, dev, s); return; }
@@ -220,7 +322,7 @@ void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device de
     if (count == 0) return;
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclAllReduce");
+        CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclAllReduce", nccl_);
         return;
     }
     if (t == DType::F16 || t == DType::BF16) { HostSum16(false, t, send, recv, count, dev, s); return; }
@@ -270,7 +372,7 @@ void Comm::Bcast(DType t, void* buf, Int count, int root, Device dev, hipStream_
     if (rank_ != root) GlobalCommStats().bytes += static_cast<int64_t>(bytes);
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclBroadcast(buf, buf, count, NcclType(t), root, nccl_, s), "ncclBroadcast");
+        CheckNccl(ncclBroadcast(buf, buf, count, NcclType(t), root, nccl_, s), "ncclBroadcast", nccl_);
         return;
     }
     if (dev == Device::CPU) { HostCall(ELX_COLL_BCAST, t, buf, buf, count, root, 0); return; }
@@ -305,10 +407,10 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
         CheckNccl(ncclGroupStart(), "ncclGroupStart");
         for (int q = 0; q < size_; ++q) {
             if (q == rank_) continue;
-            if (sc[q] > 0) CheckNccl(ncclSend(sb + sd[q] * es, sc[q], nt, q, nccl_, s), "ncclSend");
-            if (rc[q] > 0) CheckNccl(ncclRecv(rb + rd[q] * es, rc[q], nt, q, nccl_, s), "ncclRecv");
+            if (sc[q] > 0) CheckNccl(ncclSend(sb + sd[q] * es, sc[q], nt, q, nccl_, s), "ncclSend", nccl_);
+            if (rc[q] > 0) CheckNccl(ncclRecv(rb + rd[q] * es, rc[q], nt, q, nccl_, s), "ncclRecv", nccl_);
         }
-        CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+        CheckNccl(ncclGroupEnd(), "ncclGroupEnd", nccl_);
         CommProf().End(rec, s, in_bytes);
         return;
     }
@@ -342,9 +444,22 @@ void Comm::AllToAllV(DType t, const void* send, const std::vector<Int>& sc, cons
     }
 }
 
+// ELX_GROUPED_EXCHANGE=0 runs the sets of a group as separate exchanges
+bool GroupedExchange() {
+    static const bool on = [] {
+        const char* e = std::getenv("ELX_GROUPED_EXCHANGE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 void Comm::AllToAllVGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s) {
-    if (sets.size() == 1 || kind_ != Kind::RCCL || size_ == 1) {
+    if (sets.size() == 1 || size_ == 1 || !GroupedExchange()) {
         for (const VSet& v : sets) AllToAllV(v.t, v.send, *v.sc, *v.sd, v.recv, *v.rc, *v.rd, dev, s);
+        return;
+    }
+    if (kind_ == Kind::HOST) {
+        HostGroup(sets, dev, s);
         return;
     }
     ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
@@ -369,12 +484,65 @@ void Comm::AllToAllVGroup(const std::vector<VSet>& sets, Device dev, hipStream_t
         char* rb = static_cast<char*>(v.recv);
         for (int q = 0; q < size_; ++q) {
             if (q == rank_) continue;
-            if ((*v.sc)[q] > 0) CheckNccl(ncclSend(sb + (*v.sd)[q] * es, (*v.sc)[q], nt, q, nccl_, s), "ncclSend");
-            if ((*v.rc)[q] > 0) CheckNccl(ncclRecv(rb + (*v.rd)[q] * es, (*v.rc)[q], nt, q, nccl_, s), "ncclRecv");
+            if ((*v.sc)[q] > 0) CheckNccl(ncclSend(sb + (*v.sd)[q] * es, (*v.sc)[q], nt, q, nccl_, s), "ncclSend", nccl_);
+            if ((*v.rc)[q] > 0) CheckNccl(ncclRecv(rb + (*v.rd)[q] * es, (*v.rc)[q], nt, q, nccl_, s), "ncclRecv", nccl_);
         }
     }
-    CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+    CheckNccl(ncclGroupEnd(), "ncclGroupEnd", nccl_);
     CommProf().End(rec, s, in_bytes);
+}
+
+// The host backend's grouped exchange: ONE all-to-all carrying every set, each
+// peer's message the sets' portions for it concatenated in set order — the
+// order in which the RCCL branch posts its sends and receives per peer (and in
+// which RCCL matches them), with the same per-set counts and displacements.
+// 2-byte carrier units (every element size is a multiple); self portions never
+// leave the device.
+void Comm::HostGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s) {
+    constexpr size_t U = 2;
+    std::vector<Int> sc(size_, 0), rc(size_, 0), sd(size_, 0), rd(size_, 0);
+    for (const VSet& v : sets) {
+        const size_t es = DTypeSize(v.t);
+        for (int q = 0; q < size_; ++q) {
+            if (q == rank_) continue;
+            sc[q] += static_cast<Int>((*v.sc)[q] * es / U);
+            rc[q] += static_cast<Int>((*v.rc)[q] * es / U);
+        }
+        CopyBytes(dev, static_cast<char*>(v.recv) + (*v.rd)[rank_] * es,
+                  static_cast<const char*>(v.send) + (*v.sd)[rank_] * es, static_cast<size_t>((*v.rc)[rank_]) * es, s);
+    }
+    for (int q = 1; q < size_; ++q) {
+        sd[q] = sd[q - 1] + sc[q - 1];
+        rd[q] = rd[q - 1] + rc[q - 1];
+    }
+    std::vector<char> hs(static_cast<size_t>(sd[size_ - 1] + sc[size_ - 1]) * U + U);
+    std::vector<char> hr(static_cast<size_t>(rd[size_ - 1] + rc[size_ - 1]) * U + U);
+    auto move = [&](void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+        if (bytes == 0) return;
+        if (dev == Device::GPU) ELX_CHECK_HIP(hipMemcpy(dst, src, bytes, kind));
+        else std::memcpy(dst, src, bytes);
+    };
+    if (dev == Device::GPU) ELX_CHECK_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < size_; ++q) {
+        if (q == rank_) continue;
+        size_t off = static_cast<size_t>(sd[q]) * U;
+        for (const VSet& v : sets) {
+            const size_t es = DTypeSize(v.t), bytes = static_cast<size_t>((*v.sc)[q]) * es;
+            move(hs.data() + off, static_cast<const char*>(v.send) + (*v.sd)[q] * es, bytes, hipMemcpyDeviceToHost);
+            off += bytes;
+        }
+    }
+    std::vector<Int> sc0 = sc, rc0 = rc;  // self entries stay 0: handled above
+    AllToAllV(DType::F16, hs.data(), sc0, sd, hr.data(), rc0, rd, Device::CPU, nullptr);
+    for (int q = 0; q < size_; ++q) {
+        if (q == rank_) continue;
+        size_t off = static_cast<size_t>(rd[q]) * U;
+        for (const VSet& v : sets) {
+            const size_t es = DTypeSize(v.t), bytes = static_cast<size_t>((*v.rc)[q]) * es;
+            move(static_cast<char*>(v.recv) + (*v.rd)[q] * es, hr.data() + off, bytes, hipMemcpyHostToDevice);
+            off += bytes;
+        }
+    }
 }
 
 void Comm::SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s) {
@@ -390,9 +558,9 @@ void Comm::SendRecv(DType t, const void* send, int dest, void* recv, int src, In
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
         const ncclDataType_t nt = NcclType(t);
         CheckNccl(ncclGroupStart(), "ncclGroupStart");
-        CheckNccl(ncclSend(send, count, nt, dest, nccl_, s), "ncclSend");
-        CheckNccl(ncclRecv(recv, count, nt, src, nccl_, s), "ncclRecv");
-        CheckNccl(ncclGroupEnd(), "ncclGroupEnd");
+        CheckNccl(ncclSend(send, count, nt, dest, nccl_, s), "ncclSend", nccl_);
+        CheckNccl(ncclRecv(recv, count, nt, src, nccl_, s), "ncclRecv", nccl_);
+        CheckNccl(ncclGroupEnd(), "ncclGroupEnd", nccl_);
         return;
     }
     if (dev == Device::CPU) { HostCall(ELX_COLL_SENDRECV, t, send, recv, count, dest, src); return; }
@@ -411,11 +579,158 @@ void Comm::Barrier() {
         hipStream_t s = Runtime::Get().CommStream();
         static Buffer flag;
         if (!flag.data()) flag.Reset(Device::GPU, 64, nullptr);
-        CheckNccl(ncclAllReduce(flag.data(), flag.data(), 1, ncclFloat32, ncclSum, nccl_, s), "barrier");
+        CheckNccl(ncclAllReduce(flag.data(), flag.data(), 1, ncclFloat32, ncclSum, nccl_, s), "barrier", nccl_);
         ELX_CHECK_HIP(hipStreamSynchronize(s));
         return;
     }
     HostCall(ELX_COLL_BARRIER, DType::F32, nullptr, nullptr, 0, 0, 0);
+}
+
+void WatchdogStage(const char* name, double seconds) {
+    Watchdog& w = WD();
+    std::lock_guard<std::mutex> lk(w.mu);
+    w.stage = name ? name : "";
+    w.budget = seconds;
+    w.deadline = seconds > 0 ? Now() + seconds : 0;
+    std::fprintf(stderr, "[elx] stage %s%s\n", w.stage.c_str(),
+                 seconds > 0 ? Cat(" (deadline ", seconds, " s)").c_str() : "");
+    std::fflush(stderr);
+    if (!w.started) {
+        w.started = true;
+        std::thread([&w] { w.Loop(); }).detach();
+    }
+}
+
+void WatchdogEpitaph(const char* text, int exit_code) {
+    Watchdog& w = WD();
+    std::lock_guard<std::mutex> lk(w.mu);
+    w.epitaph = text ? text : "";
+    w.epitaph_code = exit_code;
+}
+
+void WatchdogRegister(ncclComm_t c) {
+    if (!c) return;
+    Watchdog& w = WD();
+    std::lock_guard<std::mutex> lk(w.mu);
+    w.comms.push_back(c);
+}
+
+void WatchdogUnregister(ncclComm_t c) {
+    Watchdog& w = WD();
+    std::lock_guard<std::mutex> lk(w.mu);
+    w.comms.erase(std::remove(w.comms.begin(), w.comms.end(), c), w.comms.end());
+}
+
+namespace {
+void SendAll(int fd, const char* p, size_t n) {
+    while (n) {
+        const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (k <= 0) throw CommError(Cat("rendezvous send failed: ", std::strerror(errno)));
+        p += k;
+        n -= static_cast<size_t>(k);
+    }
+}
+void RecvAll(int fd, char* p, size_t n, double deadline) {
+    while (n) {
+        pollfd pf{fd, POLLIN, 0};
+        const int left = static_cast<int>(std::max(0.0, deadline - Now()) * 1000);
+        if (::poll(&pf, 1, left) <= 0) throw CommError("rendezvous: timed out waiting for rank 0's data");
+        const ssize_t k = ::recv(fd, p, n, 0);
+        if (k <= 0) throw CommError("rendezvous: rank 0 closed the connection early");
+        p += k;
+        n -= static_cast<size_t>(k);
+    }
+}
+struct Fd {
+    int fd = -1;
+    ~Fd() { if (fd >= 0) ::close(fd); }
+};
+}  // namespace
+
+void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s) {
+    ELX_REQUIRE(size >= 1 && rank >= 0 && rank < size, "rendezvous: bad rank ", rank, " of ", size);
+    ELX_REQUIRE(port > 0 && port < 65536, "rendezvous: bad port ", port);
+    if (size == 1) return;
+    const double deadline = Now() + timeout_s;
+    if (rank == 0) {
+        Fd ls;
+        ls.fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        if (ls.fd < 0) throw CommError("rendezvous: socket() failed");
+        const int one = 1;
+        ::setsockopt(ls.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+        sockaddr_in sa{};
+        sa.sin_family = AF_INET;
+        sa.sin_addr.s_addr = htonl(INADDR_ANY);
+        sa.sin_port = htons(static_cast<uint16_t>(port));
+        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0)
+            throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
+        if (::listen(ls.fd, size) != 0) throw CommError("rendezvous: listen() failed");
+        for (int served = 1; served < size; ++served) {
+            pollfd pf{ls.fd, POLLIN, 0};
+            const int left = static_cast<int>(std::max(0.0, deadline - Now()) * 1000);
+            if (::poll(&pf, 1, left) <= 0)
+                throw CommError(Cat("rendezvous: only ", served - 1, " of ", size - 1, " peers connected in time"));
+            Fd peer;
+            peer.fd = ::accept(ls.fd, nullptr, nullptr);
+            if (peer.fd < 0) throw CommError("rendezvous: accept() failed");
+            SendAll(peer.fd, static_cast<const char*>(data), bytes);
+        }
+        return;
+    }
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    const std::string ps = std::to_string(port);
+    if (::getaddrinfo(addr && *addr ? addr : "127.0.0.1", ps.c_str(), &hints, &res) != 0 || !res)
+        throw CommError(Cat("rendezvous: cannot resolve ", addr));
+    std::unique_ptr<addrinfo, void (*)(addrinfo*)> guard(res, ::freeaddrinfo);
+    for (;;) {  // rank 0 may not be listening yet
+        Fd s;
+        s.fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        if (s.fd < 0) throw CommError("rendezvous: socket() failed");
+        if (::connect(s.fd, res->ai_addr, res->ai_addrlen) == 0) {
+            RecvAll(s.fd, static_cast<char*>(data), bytes, deadline);
+            return;
+        }
+        if (Now() > deadline) throw CommError(Cat("rendezvous: could not reach rank 0 at ", addr, ":", port));
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+}
+
+std::shared_ptr<Comm>& WorldComm() {
+    static std::shared_ptr<Comm> w = Comm::Self();
+    return w;
+}
+
+void InitWorldFromEnv() {
+    auto geti = [](const char* k, int dflt) {
+        const char* e = std::getenv(k);
+        return e && *e ? std::atoi(e) : dflt;
+    };
+    // launched (RANK and WORLD_SIZE set, as torch.distributed.run does): an RCCL
+    // world, one process per GPU, even of size 1; otherwise (or ELX_WORLD=self)
+    // the size-1 world
+    const char* mode = std::getenv("ELX_WORLD");
+    const bool launched = std::getenv("RANK") && std::getenv("WORLD_SIZE");
+    if (!launched || (mode && std::string(mode) == "self")) {
+        WorldComm() = Comm::Self();
+        return;
+    }
+    const int size = geti("WORLD_SIZE", 1), rank = geti("RANK", 0);
+    ELX_REQUIRE(size >= 1 && rank >= 0 && rank < size, "El::Initialize: RANK ", rank, " / WORLD_SIZE ", size);
+    Runtime::Get().SetDevice(geti("LOCAL_RANK", 0));
+    Runtime::Get().EnsureGPU();
+    const char* addr = std::getenv("MASTER_ADDR");
+    const int port = geti("ELX_RENDEZVOUS_PORT", geti("MASTER_PORT", 29499) + 1);
+    unsigned char id[128] = {};
+    if (rank == 0) {
+        ncclUniqueId uid;
+        CheckNccl(ncclGetUniqueId(&uid), "ncclGetUniqueId");
+        std::memcpy(id, uid.internal, 128);
+    }
+    RendezvousBcast(id, sizeof(id), rank, size, addr ? addr : "127.0.0.1", port,
+                    geti("ELX_RENDEZVOUS_TIMEOUT", 300));
+    WorldComm() = Comm::InitRCCL(rank, size, id);
 }
 
 }  // namespace elx

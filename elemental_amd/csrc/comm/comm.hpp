@@ -43,6 +43,27 @@ struct CommProfiler {
 };
 CommProfiler& CommProf();
 
+// Stage watchdog (replaces the fencing the reference gets from MPI's and
+// Aluminum's own error handling, include/El/core/imports/mpi/aluminum_comm.hpp:174-212):
+// a background thread that ends the process with exit code kWatchdogExit,
+// naming the stage on stderr, when the armed stage overruns its deadline or an
+// owned RCCL communicator reports an asynchronous error.  Every live owned RCCL
+// communicator is aborted first (ncclCommAbort) so no GPU kernel is left
+// spinning on a peer.  seconds <= 0 keeps the stage name but disarms the deadline.
+constexpr int kWatchdogExit = 75;
+void WatchdogStage(const char* name, double seconds);
+// text written to stdout when the watchdog fires (empty: nothing), and the exit
+// status it then uses (kWatchdogExit until set)
+void WatchdogEpitaph(const char* text, int exit_code);
+void WatchdogRegister(ncclComm_t c);
+void WatchdogUnregister(ncclComm_t c);
+
+// One-to-all byte broadcast over TCP (rank 0 serves `addr:port`): the RCCL
+// unique-id exchange MPI_Bcast does for the reference's Aluminum init, for
+// processes started by torch.distributed.run (RANK / WORLD_SIZE / MASTER_ADDR).
+void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s);
+
+
 class Comm {
 public:
     enum class Kind { SELF, RCCL, HOST };
@@ -73,7 +94,9 @@ public:
                    hipStream_t s);
     // Several AllToAllV exchanges of one communicator in ONE RCCL group (every
     // set's sends and receives posted together, so exchanges with disjoint peer
-    // sets use their links concurrently); other backends run them in order.
+    // sets use their links concurrently); the host backend carries them in one
+    // all-to-all with the same per-peer set order (ELX_GROUPED_EXCHANGE=0: the
+    // sets run as separate exchanges on either backend).
     struct VSet {
         DType t;
         const void* send;
@@ -92,6 +115,7 @@ public:
 private:
     Comm() = default;
     void HostCall(int op, DType t, const void* send, void* recv, Int count, int peer, int peer2);
+    void HostGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s);
     // 16-bit sums on the host backend, independent of what the callback supports
     // (the reference registers its own MPI_Op, src/core/environment.cpp:135-142,259-298)
     void HostSum16(bool scatter, DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
@@ -104,5 +128,10 @@ private:
     void* ctx_ = nullptr;
     int group_ = 0;
 };
+
+// The world communicator El::mpi::COMM_WORLD resolves to (size 1 until one is
+// installed); InitWorldFromEnv builds an RCCL world from the launcher's env.
+std::shared_ptr<Comm>& WorldComm();
+void InitWorldFromEnv();
 
 }  // namespace elx

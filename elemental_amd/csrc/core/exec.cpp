@@ -208,6 +208,43 @@ void Scale(Device dev, DType t, Int m, Int n, double alpha, void* A, Int lda, hi
     });
 }
 
+namespace {
+double NormMax(double a, double b) { return a != a ? a : b != b ? b : std::max(a, b); }
+// mode 0: max |a|; mode 1: sum (a / scale)^2 — device partials reduced on the host
+double NormReduce(Device dev, DType t, int mode, Int m, Int n, const void* A, Int lda, double scale, hipStream_t s) {
+    double r = 0.0;
+    if (m <= 0 || n <= 0) return r;
+    if (dev == Device::GPU) {
+        Buffer parts(Device::GPU, sizeof(double) * kern::kNormPartsMax, s);
+        int np = 0;
+        check(kern::norm_partials((int)t, mode, m, n, A, lda, scale, static_cast<double*>(parts.data()), &np, s),
+              "norm_partials");
+        std::vector<double> h(np);
+        ELX_CHECK_HIP(hipMemcpyAsync(h.data(), parts.data(), sizeof(double) * np, hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+        for (double v : h) r = mode == 0 ? NormMax(r, v) : r + v;
+        return r;
+    }
+    HOST_DTYPE_SWITCH(t, S, {
+        const S* a = static_cast<const S*>(A);
+        for (Int j = 0; j < n; ++j)
+            for (Int i = 0; i < m; ++i) {
+                const double x = (double)H<S>::ld(a + i + j * lda);
+                if (mode == 0) r = NormMax(r, std::fabs(x));
+                else { const double y = x / scale; r += y * y; }
+            }
+    });
+    return r;
+}
+}  // namespace
+
+double AbsMax(Device dev, DType t, Int m, Int n, const void* A, Int lda, hipStream_t s) {
+    return NormReduce(dev, t, 0, m, n, A, lda, 1.0, s);
+}
+double ScaledSumSq(Device dev, DType t, Int m, Int n, const void* A, Int lda, double scale, hipStream_t s) {
+    return NormReduce(dev, t, 1, m, n, A, lda, scale, s);
+}
+
 void Hadamard(Device dev, DType t, Int m, Int n, const void* A, Int lda, const void* B, Int ldb, void* C,
               Int ldc, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

@@ -20,6 +20,9 @@ void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alp
           const void* A, Int lda, const void* B, Int ldb, double beta, void* C, Int ldc, hipStream_t s);
 void Fill(Device dev, DType t, Int m, Int n, double v, void* A, Int lda, hipStream_t s);
 void Scale(Device dev, DType t, Int m, Int n, double alpha, void* A, Int lda, hipStream_t s);
+// Frobenius-norm pieces: max |a| (NaN propagates) and sum (a / scale)^2, in double
+double AbsMax(Device dev, DType t, Int m, Int n, const void* A, Int lda, hipStream_t s);
+double ScaledSumSq(Device dev, DType t, Int m, Int n, const void* A, Int lda, double scale, hipStream_t s);
 void Hadamard(Device dev, DType t, Int m, Int n, const void* A, Int lda, const void* B, Int ldb,
               void* C, Int ldc, hipStream_t s);
 void Map(Device dev, DType t, int fn, Int m, Int n, const void* A, Int lda, void* B, Int ldb, hipStream_t s);

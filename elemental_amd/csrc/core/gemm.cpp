@@ -15,8 +15,9 @@
 //    their S extra copies of C.
 //  * communication panel (Blocksize(), default 128) and compute panel are
 //    decoupled: ComputePanel() consecutive columns of A / rows of B are moved
-//    per step (K/16 clamped to [2048, 8192], whole k on a 1x1 grid where the "gathers" are
-//    local views), so the fp64 update runs at k >= 2048 instead of k = 128 and
+//    per step (EffectivePanel: K/8 for f64/f32, K/4 for f16/bf16, clamped to
+//    [2048, 8192]; whole k on a 1x1 grid where the "gathers" are local
+//    views), so the fp64 update runs at k >= 2048 instead of k = 128 and
 //    C's HBM round trip per panel stays a few % of the MFMA time.  Only the
 //    summation order changes (normwise tolerance); data movement is bit-exact.
 //  * the _MS algorithm ids are the reference's multistream variants: with a
@@ -37,7 +38,12 @@
 namespace elx {
 
 namespace {
-Int g_blocksize = 128;      // src/core/environment.cpp:315
+// the algorithmic blocksize stack (src/blas_like/blocksizes.cpp:16,38-72);
+// Initialize() leaves one entry, 128 (src/core/environment.cpp:314-315)
+std::vector<Int>& BlocksizeStack() {
+    static std::vector<Int> s{128};
+    return s;
+}
 Int g_compute_panel = 0;    // 0 = automatic
 int g_last_alg = ELX_GEMM_DEFAULT;
 constexpr Int kDotBlock = 2000;  // NN.hpp:578 (hard-coded in the reference)
@@ -286,7 +292,7 @@ int TeamCount(const DistMatrix& C, Int panels) {
 }
 
 Int EffectivePanel(const Grid& g, Int K, DType t) {
-    const Int nb = std::max<Int>(1, g_blocksize);
+    const Int nb = std::max<Int>(1, Blocksize());
     Int kc = g_compute_panel;
     // automatic: C's HBM round trip per panel (read + write, 2s bytes per
     // element) against the panel's 2*kc FLOP per element.
@@ -487,7 +493,7 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
     // (a single quarter-depth step left the second, full-depth gather exposed
     // where a panel's transfer and update take similar time: 16-bit C5 at 2x4).
     // A 1x1 grid uses its panels in place: no ramp.
-    const Int nb = std::max<Int>(1, g_blocksize);
+    const Int nb = std::max<Int>(1, Blocksize());
     std::vector<Int> kb{0};
     if (g.Size() > 1 && kc >= 4 * nb && K > kc) {
         for (Int d : {kc / 4, kc / 2}) {
@@ -679,7 +685,7 @@ void SummaA(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
-    const Int n = Cp.Get().Width(), nb = std::max<Int>(1, g_blocksize);
+    const Int n = Cp.Get().Width(), nb = std::max<Int>(1, Blocksize());
     TeamViews tv(*Ap, *Bp, Cp.Get(), ms ? TeamCount(Cp.Get(), (n + nb - 1) / nb) : 1);
     for (Int k = 0; k < n; k += nb) {
         const auto& tm = tv[k / nb];
@@ -725,7 +731,7 @@ void SummaB(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
     auto Ap = ReadProxy(APre, CPre, Dist::MC, Dist::MR);
     auto Bp = ReadProxy(BPre, CPre, Dist::MC, Dist::MR);
     RWProxy Cp(CPre);
-    const Int m = Cp.Get().Height(), nb = std::max<Int>(1, g_blocksize);
+    const Int m = Cp.Get().Height(), nb = std::max<Int>(1, Blocksize());
     TeamViews tv(*Ap, *Bp, Cp.Get(), ms ? TeamCount(Cp.Get(), (m + nb - 1) / nb) : 1);
     for (Int k = 0; k < m; k += nb) {
         const auto& tm = tv[k / nb];
@@ -869,8 +875,25 @@ int Heuristic(Int m, Int n, Int k) {  // NN.hpp:583-600 (same weights in NT/TN/T
 
 }  // namespace
 
-void SetBlocksize(Int nb) { ELX_REQUIRE(nb > 0, "blocksize must be positive"); g_blocksize = nb; }
-Int Blocksize() { return g_blocksize; }
+// an empty stack is a LogicError here (the reference checks it in debug builds only)
+void SetBlocksize(Int nb) {
+    ELX_REQUIRE(nb > 0, "blocksize must be positive");
+    ELX_REQUIRE(!BlocksizeStack().empty(), "Attempted to set blocksize at top of empty stack");
+    BlocksizeStack().back() = nb;
+}
+Int Blocksize() {
+    ELX_REQUIRE(!BlocksizeStack().empty(), "Attempted to extract blocksize from empty stack");
+    return BlocksizeStack().back();
+}
+void PushBlocksizeStack(Int nb) {
+    ELX_REQUIRE(nb > 0, "blocksize must be positive");
+    BlocksizeStack().push_back(nb);
+}
+void PopBlocksizeStack() {
+    ELX_REQUIRE(!BlocksizeStack().empty(), "Attempted to pop an empty blocksize stack");
+    BlocksizeStack().pop_back();
+}
+void EmptyBlocksizeStack() { BlocksizeStack().clear(); }
 void SetComputePanel(Int kc) { ELX_REQUIRE(kc >= 0, "compute panel must be >= 0"); g_compute_panel = kc; }
 Int ComputePanel() { return g_compute_panel; }
 int LastGemmAlgorithm() { return g_last_alg; }
@@ -1069,7 +1092,7 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     RWProxy Xp(XPre);
     DistMatrix& X = Xp.Get();
     const Int m = X.Height(), n = X.Width();
-    Int nb = std::max<Int>(1, g_blocksize);
+    Int nb = std::max<Int>(1, Blocksize());
     const bool trans = orient != ELX_NORMAL, lower = uplo == ELX_LOWER;
     const bool forward = lower != trans;  // op(A) lower: blocks top to bottom
     auto A11s = A.Like(Dist::STAR, Dist::STAR);
@@ -1106,6 +1129,7 @@ void TrsmLeft(int uplo, int orient, bool unit, const DistMatrix& APre, DistMatri
     auto batch_ok = [&](Int b) {
         return X.Dev() == Device::GPU && SameLocalLayout(A, Dist::STAR, Dist::STAR, 0, 0) &&
                b * 65 * (Int)es <= kern::kTriInverseLdsMax && (m + b - 1) / b <= 65535 &&
+               kern::tri_inverse_lds_ok(static_cast<int>(X.Type()), b) &&
                SameLocalLayout(X, Dist::STAR, Dist::VR, 0, X.RowAlign()) && X.LocalWidth() >= 4 * b;
     };
     // Batched path with the default Blocksize (128) and a large system: 256-row

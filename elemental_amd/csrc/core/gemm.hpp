@@ -33,6 +33,9 @@ void Symm(int side, int uplo, double alpha, const DistMatrix& A, const DistMatri
 
 void SetBlocksize(Int nb);
 Int Blocksize();
+void PushBlocksizeStack(Int nb);
+void PopBlocksizeStack();
+void EmptyBlocksizeStack();
 void SetComputePanel(Int kc);
 Int ComputePanel();
 int LastGemmAlgorithm();

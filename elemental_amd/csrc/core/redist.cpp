@@ -580,6 +580,27 @@ double GridAllReduceSum(const Grid& g, double v) {
     return ScalarColl(g, v, [&](void* p, Device d, hipStream_t s) { g.VC().AllReduce(DType::F64, p, p, 1, d, s); });
 }
 
+// max over the grid (NaN wins): every rank's value gathered over VC
+double GridAllReduceMax(const Grid& g, double v) {
+    const int p = g.Size();
+    if (p == 1) return v;
+    std::vector<double> all(p);
+    if (g.CommDevice() == Device::GPU) {
+        hipStream_t s = Runtime::Get().CommStream();
+        elx::Buffer b(Device::GPU, sizeof(double) * (p + 1), s);
+        double* d = static_cast<double*>(b.data());
+        ELX_CHECK_HIP(hipMemcpyAsync(d, &v, sizeof(double), hipMemcpyHostToDevice, s));
+        g.VC().AllGather(DType::F64, d, d + 1, 1, Device::GPU, s);
+        ELX_CHECK_HIP(hipMemcpyAsync(all.data(), d + 1, sizeof(double) * p, hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+    } else {
+        g.VC().AllGather(DType::F64, &v, all.data(), 1, Device::CPU, nullptr);
+    }
+    double r = all[0];
+    for (double x : all) r = r != r ? r : x != x ? x : std::max(r, x);
+    return r;
+}
+
 double GridBcast(const Grid& g, double v, int rootVC) {
     return ScalarColl(g, v, [&](void* p, Device d, hipStream_t s) { g.VC().Bcast(DType::F64, p, 1, rootVC, d, s); });
 }
@@ -617,29 +638,32 @@ void Fill(DistMatrix& A, double v) {
     exec::Fill(A.Dev(), A.Type(), A.LocalHeight(), A.LocalWidth(), v, A.Buffer(), A.LDim(), A.Stream());
 }
 
-// Trsm's checkIfSingular (src/blas_like/level3/Trsm.cpp:60-68): is any diagonal
-// entry of A exactly zero?  The local diagonal entries form one arithmetic
-// progression (global index step lcm(colStride, rowStride)), gathered by one
-// strided copy; the per-rank answers are summed over the grid.
+// El::FrobeniusNorm (src/lapack_like/props/Norm/Frobenius.cpp:20-60): the
+// reference's scaled sum of squares (UpdateScaledSquare) with one scale, the
+// grid-wide max |a|, so no entry overflows or underflows the squares; both
+// passes are device reductions over the local block.  Replicated copies of a
+// local block (e.g. [STAR,STAR]) count once.
 double FrobeniusNorm(const DistMatrix& A) {
-    double local = 0.0;
     const Int lh = A.LocalHeight(), lw = A.LocalWidth();
-    if (A.Participating() && lh > 0 && lw > 0) {
-        const size_t es = A.ElemSize();
-        std::vector<unsigned char> host((size_t)lh * lw * es);
-        A.GetLocal(host.data(), lh);
-        for (size_t q = 0; q < (size_t)lh * lw; ++q) {
-            const double v = exec::LoadScalar(A.Type(), host.data() + q * es);
-            local += v * v;
-        }
+    const bool mine = A.Participating() && lh > 0 && lw > 0;
+    const double amax = GridAllReduceMax(
+        A.G(), mine ? exec::AbsMax(A.Dev(), A.Type(), lh, lw, A.Buffer(), A.LDim(), A.Stream()) : 0.0);
+    if (amax == 0.0 || !std::isfinite(amax)) return amax;
+    double local = 0.0;
+    if (mine) {
+        local = exec::ScaledSumSq(A.Dev(), A.Type(), lh, lw, A.Buffer(), A.LDim(), amax, A.Stream());
         int copies = 0;  // ranks holding this same local block (replicated distributions)
         for (int q = 0; q < A.G().Size(); ++q)
             if (A.ColRankOf(q) == A.ColRank() && A.RowRankOf(q) == A.RowRank()) ++copies;
         local /= copies;
     }
-    return std::sqrt(GridAllReduceSum(A.G(), local));
+    return amax * std::sqrt(GridAllReduceSum(A.G(), local));
 }
 
+// Trsm's checkIfSingular (src/blas_like/level3/Trsm.cpp:60-68): is any diagonal
+// entry of A exactly zero?  The local diagonal entries form one arithmetic
+// progression (global index step lcm(colStride, rowStride)), gathered by one
+// strided copy; the per-rank answers are summed over the grid.
 bool DiagonalHasZero(const DistMatrix& A) {
     const Int n = std::min(A.Height(), A.Width());
     double zeros = 0;

@@ -44,6 +44,7 @@ bool DiagonalHasZero(const DistMatrix& A);
 double FrobeniusNorm(const DistMatrix& A);
 // grid-wide scalar sum / broadcast from VC rank `rootVC`
 double GridAllReduceSum(const Grid& g, double v);
+double GridAllReduceMax(const Grid& g, double v);
 double GridBcast(const Grid& g, double v, int rootVC);
 
 }  // namespace elx

@@ -587,6 +587,41 @@ bool TransposeViaLds() {
     return v;
 }
 
+// Frobenius-norm partials in double, one per workgroup: MODE 0 the largest
+// |a| (NaN wins), MODE 1 the sum of (a / scale)^2 (El::FrobeniusNorm's scaled
+// sum of squares, src/lapack_like/props/Norm/Frobenius.cpp:37-44, with the
+// grid-wide max as the one scale)
+__device__ __forceinline__ double norm_max(double a, double b) { return a != a ? a : b != b ? b : (a > b ? a : b); }
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(NT) void norm_partial_kernel(i64 m, i64 n, const typename Elem<T>::storage* A, i64 lda,
+                                                          double scale, double* out) {
+    using E = Elem<T>;
+    double acc = 0.0;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        for (i64 i = (i64)blockIdx.x * NT + threadIdx.x; i < m; i += (i64)gridDim.x * NT) {
+            const double x = (double)E::load(A[i + j * lda]);
+            if (MODE == 0) {
+                acc = norm_max(acc, x < 0 ? -x : x);
+            } else {
+                const double y = x / scale;
+                acc += y * y;
+            }
+        }
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(acc, off, 64);
+        acc = MODE == 0 ? norm_max(acc, o) : acc + o;
+    }
+    __shared__ double wave[NT / 64];
+    if ((threadIdx.x & 63) == 0) wave[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = wave[0];
+        for (int w = 1; w < NT / 64; ++w) r = MODE == 0 ? norm_max(r, wave[w]) : r + wave[w];
+        out[(i64)blockIdx.y * gridDim.x + blockIdx.x] = r;
+    }
+}
+
 }  // namespace
 
 hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s, int max_wgs) {
@@ -664,6 +699,24 @@ hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream
         const EwShape g = ew_shape<typename Elem<T>::storage>(m, n, {{A, lda}});
         hipLaunchKernelGGL((fill_kernel<T>), g.grid, dim3(NT), 0, s, g.m, g.n, v,
                            static_cast<typename Elem<T>::storage*>(A), lda, g.vec);
+    });
+    return hipGetLastError();
+}
+
+hipError_t norm_partials(int dtype, int mode, i64 m, i64 n, const void* A, i64 lda, double scale, double* out,
+                         int* nparts, hipStream_t s) {
+    *nparts = 0;
+    if (m <= 0 || n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)std::min<i64>((m + NT - 1) / NT, 32), (unsigned)std::min<i64>(n, kNormPartsMax / 32));
+    *nparts = (int)(grid.x * grid.y);
+    ELX_DTYPE_SWITCH(dtype, T, {
+        using S = typename Elem<T>::storage;
+        if (mode == 0)
+            hipLaunchKernelGGL((norm_partial_kernel<T, 0>), grid, dim3(NT), 0, s, m, n, static_cast<const S*>(A), lda,
+                               scale, out);
+        else
+            hipLaunchKernelGGL((norm_partial_kernel<T, 1>), grid, dim3(NT), 0, s, m, n, static_cast<const S*>(A), lda,
+                               scale, out);
     });
     return hipGetLastError();
 }

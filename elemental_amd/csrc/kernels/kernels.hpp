@@ -86,6 +86,11 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
 // Type-converting strided copy: dst(i,j) = (dst type) src(i,j), one rounding (elem.hpp).
 hipError_t convert2d(int src_dtype, int dst_dtype, const Copy2D& d, hipStream_t s);
 hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s);
+// Frobenius-norm partials (mode 0: max |a|, mode 1: sum (a/scale)^2) in double,
+// at most kNormPartsMax of them written to out; *nparts says how many
+constexpr int kNormPartsMax = 4096;
+hipError_t norm_partials(int dtype, int mode, i64 m, i64 n, const void* A, i64 lda, double scale, double* out,
+                         int* nparts, hipStream_t s);
 hipError_t scale2d(int dtype, i64 m, i64 n, double alpha, void* A, i64 lda, hipStream_t s);
 hipError_t hadamard2d(int dtype, i64 m, i64 n, const void* A, i64 lda, const void* B, i64 ldb,
                       void* C, i64 ldc, hipStream_t s);
@@ -104,9 +109,12 @@ hipError_t trapezoid2d(int dtype, bool lower, i64 m, i64 n, double alpha, const 
 hipError_t trsm_local(int dtype, bool ident, bool lower, bool trans, bool unit, i64 m, i64 n, const void* A, i64 lda,
                       void* B, i64 ldb, hipStream_t s);
 // W_b := op(A_bb)^-1 for every nb x nb diagonal block of A (m x m; the last may be
-// ragged), W_b at W + b*nb*nb with leading dimension nb; one launch.  nb*65*es <= 66 KiB.
-// dynamic LDS of one tri_inverse_batched workgroup: nb x 65 elements
+// ragged), W_b at W + b*nb*nb with leading dimension nb; one launch.  Dynamic LDS
+// of one workgroup: nb x 65 elements, at most kTriInverseLdsMax (the caller
+// falls back to 128-row blocks when the >64 KiB attribute cannot be set)
 constexpr long kTriInverseLdsMax = 150 * 1024;
+// can one workgroup get nb x 65 elements of dynamic LDS (sets the >64 KiB attribute)?
+bool tri_inverse_lds_ok(int dtype, i64 nb);
 hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64 nb, i64 m, const void* A, i64 lda,
                                void* W, hipStream_t s);
 }  // namespace kern

@@ -114,6 +114,16 @@ hipError_t launch_trsm(bool ident, bool lower, bool trans, bool unit, i64 m, i64
 
 }  // namespace
 
+bool tri_inverse_lds_ok(int dtype, i64 nb) {
+    const int es = dtype == ELX_F64 ? 8 : 4;
+    const size_t lds = (size_t)nb * (WAVE + 1) * es;
+    if (lds > (size_t)kTriInverseLdsMax || (dtype != ELX_F64 && dtype != ELX_F32)) return false;
+    if (lds <= 64 * 1024) return true;
+    const void* f = dtype == ELX_F64 ? reinterpret_cast<const void*>(&tri_inverse_batched_kernel<double>)
+                                     : reinterpret_cast<const void*>(&tri_inverse_batched_kernel<float>);
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+}
+
 hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64 nb, i64 m, const void* A, i64 lda,
                                void* W, hipStream_t s) {
     if (m <= 0 || nb <= 0) return hipSuccess;
@@ -124,16 +134,20 @@ hipError_t tri_inverse_batched(int dtype, bool lower, bool trans, bool unit, i64
     const dim3 grid((unsigned)((nb + WAVE - 1) / WAVE), (unsigned)nblk);
     switch (dtype) {
     case ELX_F64:
-        if (lds > 64 * 1024)  // beyond the default dynamic-LDS limit (gfx950: 160 KiB per workgroup)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<double>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950: 160 KiB per workgroup)
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<double>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL((tri_inverse_batched_kernel<double>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
                            static_cast<const double*>(A), lda, static_cast<double*>(W));
         break;
     case ELX_F32:
-        if (lds > 64 * 1024)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<float>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (lds > 64 * 1024) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tri_inverse_batched_kernel<float>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL((tri_inverse_batched_kernel<float>), grid, dim3(WAVE), lds, s, lower, trans, unit, nb, m,
                            static_cast<const float*>(A), lda, static_cast<float*>(W));
         break;

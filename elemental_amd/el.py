@@ -23,7 +23,8 @@ from ._lib import (ADJOINT, BF16, CIRC, COLUMN_MAJOR, CPU, F16, F32, F64, GEMM_C
 __all__ = [
     "Comm", "Grid", "DistMatrix", "Gemm", "LocalGemm", "Axpy", "Scale", "Zero", "Fill", "Hadamard",
     "EntrywiseMap", "Combine", "AxpyContract", "InitializeRandom", "Uniform", "Transpose", "SetBlocksize",
-    "Blocksize", "SetComputePanel", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "Symm", "Hemm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
+    "Blocksize", "PushBlocksizeStack", "PopBlocksizeStack", "EmptyBlocksizeStack", "Initialize", "Finalize",
+    "SetComputePanel", "FrobeniusNorm", "Syrk", "Herk", "Syr2k", "Her2k", "Trrk", "Trsm", "Symm", "Hemm", "ScaleTrapezoid", "LEFT", "RIGHT", "NON_UNIT", "UNIT", "LOWER", "UPPER",
     "NORMAL", "TRANSPOSE", "ADJOINT", "MC", "MD", "MR", "VC", "VR", "STAR", "CIRC", "CPU", "GPU",
     "F32", "F64", "F16", "BF16", "GEMM_DEFAULT", "GEMM_SUMMA_A", "GEMM_SUMMA_A_MS", "GEMM_SUMMA_B",
     "GEMM_SUMMA_B_MS", "GEMM_SUMMA_C", "GEMM_SUMMA_C_MS", "GEMM_SUMMA_DOT", "GEMM_CANNON",
@@ -78,6 +79,17 @@ class Comm:
         buf = (c_ubyte * 128).from_buffer_copy(uid)
         call("elx_comm_init_rccl", byref(h), rank, size, buf)
         return cls(h)
+
+    @classmethod
+    def world(cls) -> "Comm":
+        """El::mpi::COMM_WORLD: the library's world communicator (borrowed)."""
+        h = c_void_p()
+        call("elx_comm_world", byref(h))
+        return cls(h)
+
+    def install_as_world(self):
+        """Make this communicator the one COMM_WORLD names."""
+        call("elx_comm_set_world", self.h)
 
     @classmethod
     def host(cls, bridge) -> "Comm":
@@ -430,7 +442,64 @@ def SetBlocksize(nb: int):
 
 
 def Blocksize() -> int:
-    return lib().elx_blocksize()
+    nb = lib().elx_blocksize()
+    if nb < 0:
+        raise L.LogicError(L.ERR_LOGIC, lib().elx_last_error().decode(errors="replace"))
+    return nb
+
+
+def PushBlocksizeStack(nb: int):
+    call("elx_push_blocksize", nb)
+
+
+def PopBlocksizeStack():
+    call("elx_pop_blocksize")
+
+
+def EmptyBlocksizeStack():
+    call("elx_empty_blocksize_stack")
+
+
+def Initialize():
+    """El::Initialize: world communicator from RANK / WORLD_SIZE / LOCAL_RANK /
+    MASTER_ADDR (RCCL; size 1 without them), blocksize stack {128}, RNG seeded."""
+    call("elx_initialize")
+
+
+def Finalize():
+    call("elx_finalize")
+
+
+def watchdog_stage(name: str, seconds: float = 0.0):
+    """Arm the stage watchdog: past `seconds` (or on an asynchronous RCCL error)
+    every owned RCCL communicator is aborted and the process exits with
+    WATCHDOG_EXIT, naming the stage on stderr; seconds <= 0 disarms."""
+    call("elx_watchdog_stage", name.encode(), float(seconds))
+
+
+WATCHDOG_EXIT = 75
+
+
+def watchdog_epitaph(text: str | None, exit_code: int = WATCHDOG_EXIT):
+    """Text the watchdog prints to stdout before exiting, and its exit status then."""
+    call("elx_watchdog_epitaph", (text or "").encode(), int(exit_code))
+
+
+def rendezvous_bcast(data: bytes | None, nbytes: int, rank: int, size: int, addr: str, port: int,
+                     timeout: float = 60.0) -> bytes:
+    """Rank 0's `data` (nbytes) to every rank over TCP (rank 0 listens on port)."""
+    buf = (c_ubyte * nbytes)()
+    if rank == 0:
+        ctypes.memmove(buf, data, nbytes)
+    call("elx_rendezvous_bcast", buf, nbytes, rank, size, addr.encode(), port, float(timeout))
+    return bytes(buf)
+
+
+def FrobeniusNorm(A: DistMatrix) -> float:
+    """El::FrobeniusNorm (collective over A's grid; scaled sum of squares)."""
+    v = c_double()
+    call("elx_dm_frobenius_norm", A.h, byref(v))
+    return v.value
 
 
 def SetComputePanel(kc: int):

@@ -4,7 +4,8 @@
 // include/El/core/DistMatrix/*, include/El/blas_like/level3.hpp:20-90,
 // include/El/blas_like/level1/*) so LBANN-style callers recompile against it:
 //
-//   El::Grid g(El::mpi::COMM_WORLD());            // or a communicator over RCCL / a host bridge
+//   El::Initialize(argc, argv);                  // RCCL world from RANK / WORLD_SIZE (torchrun)
+//   El::Grid g(El::mpi::COMM_WORLD);              // or a communicator over RCCL / a host bridge
 //   El::DistMatrix<double, El::MC, El::MR, El::ELEMENT, El::Device::GPU> A(m, k, g), B(k, n, g), C(m, n, g);
 //   El::Gemm(El::NORMAL, El::NORMAL, 1.0, A, B, 0.0, C);
 //
@@ -13,16 +14,196 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <initializer_list>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "elemental_amd.h"
 
+// HIP's handle types, declared exactly as hip_runtime_api.h does, so this
+// header needs no HIP include and mixes with one.
+typedef struct ihipStream_t* hipStream_t;
+typedef struct ihipEvent_t* hipEvent_t;
+
+// ---- hydrogen: devices, SyncInfo, MultiSync ------------------------------------
+// include/hydrogen/Device.hpp, SyncInfoBase.hpp, SynchronizeAPI.hpp,
+// MultiSync.hpp:33-78, device/gpu/rocm/SyncInfo.hpp:15-81, device/GPU.hpp:130-160
+namespace hydrogen {
+
+enum class Device : unsigned char { CPU = ELX_DEVICE_CPU, GPU = ELX_DEVICE_GPU };
+
+// 16-bit element types: gpu_half_type (rocblas_half in the reference,
+// include/hydrogen/utils/HalfPrecision.hpp:123) and bfloat16 (new).
+struct gpu_half_type { std::uint16_t x; };
+struct bfloat16 { std::uint16_t x; };
+
+struct GPUError : std::runtime_error { using std::runtime_error::runtime_error; };  // hydrogen::GPUError
+
+namespace detail {
+[[noreturn]] inline void ThrowGPU() { throw GPUError(elx_last_error()); }
+inline void CheckGPU(int rc) { if (rc != ELX_OK) ThrowGPU(); }
+}  // namespace detail
+
+template <Device D> class SyncInfo;
+
+// CPU work is synchronous with the host: nothing to carry
+template <> class SyncInfo<Device::CPU> {
+public:
+    SyncInfo() noexcept = default;
+};
+
+// a HIP stream and an event recorded on it to mark sync points
+template <> class SyncInfo<Device::GPU> {
+public:
+    SyncInfo();  // the library's default stream and event
+    SyncInfo(hipStream_t stream, hipEvent_t event) noexcept : stream_(stream), event_(event) {}
+    // take the other's non-null parts (SyncInfo.hpp:27-33)
+    void Merge(SyncInfo const& si) noexcept {
+        if (si.stream_) stream_ = si.stream_;
+        if (si.event_) event_ = si.event_;
+    }
+    hipStream_t Stream() const noexcept { return stream_; }
+    hipEvent_t Event() const noexcept { return event_; }
+
+private:
+    friend void DestroySyncInfo(SyncInfo<Device::GPU>&);
+    hipStream_t stream_ = nullptr;
+    hipEvent_t event_ = nullptr;
+};
+
+inline bool operator==(SyncInfo<Device::CPU> const&, SyncInfo<Device::CPU> const&) { return true; }
+inline bool operator!=(SyncInfo<Device::CPU> const&, SyncInfo<Device::CPU> const&) { return false; }
+inline bool operator==(SyncInfo<Device::GPU> const& a, SyncInfo<Device::GPU> const& b) {
+    return a.Stream() == b.Stream() && a.Event() == b.Event();
+}
+inline bool operator!=(SyncInfo<Device::GPU> const& a, SyncInfo<Device::GPU> const& b) { return !(a == b); }
+template <Device D1, Device D2> bool operator==(SyncInfo<D1> const&, SyncInfo<D2> const&) { return false; }
+template <Device D1, Device D2> bool operator!=(SyncInfo<D1> const&, SyncInfo<D2> const&) { return true; }
+
+namespace gpu {
+// the SyncInfo Hydrogen uses by default: the library's compute stream (not the
+// HIP null stream) and its event (GPU.hpp:130-144)
+inline SyncInfo<Device::GPU> const& DefaultSyncInfo() {
+    static const SyncInfo<Device::GPU> si = [] {
+        void* s = nullptr;
+        void* e = nullptr;
+        detail::CheckGPU(elx_default_stream(&s));
+        detail::CheckGPU(elx_default_event(&e));
+        return SyncInfo<Device::GPU>(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e));
+    }();
+    return si;
+}
+}  // namespace gpu
+
+inline SyncInfo<Device::GPU>::SyncInfo() : SyncInfo(gpu::DefaultSyncInfo()) {}
+
+// a new non-blocking stream and a new event (CPU: empty)
+template <Device D> SyncInfo<D> CreateNewSyncInfo();
+template <> inline SyncInfo<Device::CPU> CreateNewSyncInfo<Device::CPU>() { return SyncInfo<Device::CPU>{}; }
+template <> inline SyncInfo<Device::GPU> CreateNewSyncInfo<Device::GPU>() {
+    void* s = nullptr;
+    void* e = nullptr;
+    detail::CheckGPU(elx_stream_create(&s));
+    if (elx_event_create(&e) != ELX_OK) {
+        (void)elx_stream_destroy(s);
+        detail::ThrowGPU();
+    }
+    return SyncInfo<Device::GPU>(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e));
+}
+inline void DestroySyncInfo(SyncInfo<Device::CPU>&) noexcept {}
+inline void DestroySyncInfo(SyncInfo<Device::GPU>& si) {
+    if (si.stream_) detail::CheckGPU(elx_stream_destroy(si.stream_));
+    if (si.event_) detail::CheckGPU(elx_event_destroy(si.event_));
+    si.stream_ = nullptr;
+    si.event_ = nullptr;
+}
+
+// block the host until the SyncInfo's queued work is done
+inline void Synchronize(SyncInfo<Device::CPU> const&) {}
+inline void Synchronize(SyncInfo<Device::GPU> const& si) { detail::CheckGPU(elx_stream_synchronize(si.Stream())); }
+
+// mark this point of the SyncInfo's stream
+inline void AddSynchronizationPoint(SyncInfo<Device::CPU> const&) {}
+inline void AddSynchronizationPoint(SyncInfo<Device::GPU> const& si) {
+    detail::CheckGPU(elx_event_record(si.Event(), si.Stream()));
+}
+
+namespace details {
+// `dependent` waits for the work captured at master's last sync point
+inline void AddSyncPoint(SyncInfo<Device::CPU> const&, SyncInfo<Device::CPU> const&) {}
+inline void AddSyncPoint(SyncInfo<Device::CPU> const&, SyncInfo<Device::GPU> const&) {}
+inline void AddSyncPoint(SyncInfo<Device::GPU> const& master, SyncInfo<Device::CPU> const&) { Synchronize(master); }
+inline void AddSyncPoint(SyncInfo<Device::GPU> const& master, SyncInfo<Device::GPU> const& other) {
+    if (master.Stream() != other.Stream()) detail::CheckGPU(elx_stream_wait_event(other.Stream(), master.Event()));
+}
+}  // namespace details
+
+// the "others" wait for the master (SynchronizeAPI.hpp)
+template <Device D, Device... Ds>
+void AddSynchronizationPoint(SyncInfo<D> const& master, SyncInfo<Ds> const&... others) {
+    AddSynchronizationPoint(master);
+    int dummy[] = {0, (details::AddSyncPoint(master, others), 0)...};
+    (void)dummy;
+}
+template <Device D, Device... Ds>
+void AllWaitOnMaster(SyncInfo<D> const& master, SyncInfo<Ds> const&... others) {
+    AddSynchronizationPoint(master, others...);
+}
+template <Device D, Device... Ds>
+void MasterWaitOnAll(SyncInfo<D> const& master, SyncInfo<Ds> const&... others) {
+    int dummy[] = {0, (AddSynchronizationPoint(others, master), 0)...};
+    (void)dummy;
+}
+
+// RAII: construction makes the first (master) SyncInfo wait on the others,
+// destruction makes the others wait on the master (MultiSync.hpp:33-78)
+template <Device... Ds>
+class MultiSync {
+    using tuple_type = std::tuple<SyncInfo<Ds>...>;
+    using master_type = typename std::tuple_element<0, tuple_type>::type;
+
+public:
+    explicit MultiSync(SyncInfo<Ds> const&... sis) : sis_{sis...} { MasterWaitOnAll(sis...); }
+    ~MultiSync() { Release(std::make_index_sequence<sizeof...(Ds)>{}); }
+    MultiSync(MultiSync&& o) noexcept : sis_(o.sis_) { o.moved_ = true; }
+    MultiSync(MultiSync const&) = delete;
+    MultiSync& operator=(MultiSync const&) = delete;
+    operator master_type const&() const noexcept { return std::get<0>(sis_); }
+
+private:
+    template <std::size_t... Is>
+    void Release(std::index_sequence<Is...>) {
+        if (!moved_) AllWaitOnMaster(std::get<Is>(sis_)...);
+    }
+    tuple_type sis_;
+    bool moved_ = false;
+};
+template <Device... Ds>
+MultiSync<Ds...> MakeMultiSync(SyncInfo<Ds> const&... sis) {
+    return MultiSync<Ds...>(sis...);
+}
+
+}  // namespace hydrogen
+
 namespace El {
 
 using Int = std::int64_t;
+// the reference brings hydrogen's names into El (include/El/core.hpp:74-79)
+using hydrogen::Device;
+using hydrogen::SyncInfo;
+using hydrogen::MultiSync;
+using hydrogen::MakeMultiSync;
+using hydrogen::CreateNewSyncInfo;
+using hydrogen::DestroySyncInfo;
+using hydrogen::Synchronize;
+using hydrogen::AddSynchronizationPoint;
+using hydrogen::gpu_half_type;
+using hydrogen::bfloat16;
+namespace gpu = hydrogen::gpu;
 
 // ---- enums (ordinals match the reference) --------------------------------
 enum Dist { MC = ELX_MC, MD = ELX_MD, MR = ELX_MR, VC = ELX_VC, VR = ELX_VR, STAR = ELX_STAR, CIRC = ELX_CIRC };
@@ -37,21 +218,15 @@ enum GemmAlgorithm {
     GEMM_SUMMA_B_MS = ELX_GEMM_SUMMA_B_MS, GEMM_SUMMA_B = ELX_GEMM_SUMMA_B, GEMM_SUMMA_C_MS = ELX_GEMM_SUMMA_C_MS,
     GEMM_SUMMA_C = ELX_GEMM_SUMMA_C, GEMM_SUMMA_DOT = ELX_GEMM_SUMMA_DOT, GEMM_CANNON = ELX_GEMM_CANNON
 };
-enum class Device : unsigned char { CPU = ELX_DEVICE_CPU, GPU = ELX_DEVICE_GPU };
 // include/El/core/types.hpp:543-559 (the formats of the GEMM path's fixtures)
 enum FileFormat { AUTO = ELX_FILE_AUTO, BINARY = ELX_FILE_BINARY, BINARY_FLAT = ELX_FILE_BINARY_FLAT };
-
-// 16-bit element types: gpu_half_type (rocblas_half in the reference,
-// include/hydrogen/utils/HalfPrecision.hpp:123) and bfloat16 (new).
-struct gpu_half_type { std::uint16_t x; };
-struct bfloat16 { std::uint16_t x; };
 
 // ---- errors: the reference's exception types ------------------------------
 struct LogicError : std::logic_error { using std::logic_error::logic_error; };
 struct RuntimeError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct UnsupportedError : LogicError { using LogicError::LogicError; };
 namespace hydrogen_errors {
-struct GPUError : std::runtime_error { using std::runtime_error::runtime_error; };  // hydrogen::GPUError
+using hydrogen::GPUError;  // the round-2 spelling
 }
 // include/El/core/environment/decl.hpp:209-214
 struct SingularMatrixException : std::runtime_error {
@@ -66,7 +241,7 @@ inline void Check(int rc) {
     case ELX_ERR_LOGIC: throw LogicError(msg);
     case ELX_ERR_UNSUPPORTED: throw UnsupportedError(msg);
     case ELX_ERR_HIP:
-    case ELX_ERR_NO_DEVICE: throw hydrogen_errors::GPUError(msg);
+    case ELX_ERR_NO_DEVICE: throw hydrogen::GPUError(msg);
     case ELX_ERR_SINGULAR: throw SingularMatrixException(msg.c_str());
     default: throw RuntimeError(msg);
     }
@@ -133,7 +308,7 @@ class Comm {
 public:
     Comm() = default;
     explicit Comm(elx_comm_t c) : c_(c, [](elx_comm_s* p) { if (p) elx_comm_destroy(p); }) {}
-    // size-1 communicator (also what Grid() uses by default)
+    // size-1 communicator (COMM_SELF)
     static Comm Self() {
         elx_comm_t c = nullptr;
         detail::Check(elx_comm_init_host(&c, 0, 1, nullptr, nullptr, nullptr));
@@ -151,19 +326,38 @@ public:
         detail::Check(elx_comm_wrap_rccl(&c, ncclComm));
         return Comm(c);
     }
-    int Rank() const { int r = 0; detail::Check(elx_comm_rank(c_.get(), &r)); return r; }
-    int Size() const { int s = 1; detail::Check(elx_comm_size(c_.get(), &s)); return s; }
-    elx_comm_t Handle() const { return c_.get(); }
+    // the world communicator (what COMM_WORLD names), resolved when used
+    struct WorldTag {};
+    explicit Comm(WorldTag) noexcept : world_(true) {}
+    int Rank() const { int r = 0; detail::Check(elx_comm_rank(Handle(), &r)); return r; }
+    int Size() const { int s = 1; detail::Check(elx_comm_size(Handle(), &s)); return s; }
+    elx_comm_t Handle() const {
+        if (!world_) return c_.get();
+        elx_comm_t w = nullptr;  // borrowed from the library
+        detail::Check(elx_comm_world(&w));
+        return w;
+    }
+    // make this communicator the world (what COMM_WORLD and Grid() then use)
+    void InstallAsWorld() const { detail::Check(elx_comm_set_world(Handle())); }
 private:
     std::shared_ptr<elx_comm_s> c_;
+    bool world_ = false;
 };
+// El::mpi::COMM_WORLD / COMM_SELF (include/El/core/imports/mpi.hpp:84-86): the
+// world is the library's (El::Initialize builds it; Comm::InstallAsWorld
+// replaces it), COMM_SELF a size-1 communicator
+inline const Comm COMM_WORLD{Comm::WorldTag{}};
 inline Comm COMM_SELF() { return Comm::Self(); }
+inline int Rank(const Comm& comm = COMM_WORLD) { return comm.Rank(); }
+inline int Size(const Comm& comm = COMM_WORLD) { return comm.Size(); }
+inline void Barrier(const Comm& comm = COMM_WORLD) { detail::Check(elx_comm_barrier(comm.Handle())); }
 }  // namespace mpi
 
 // ---- El::Grid (src/core/Grid.cpp) --------------------------------------------
 class Grid {
 public:
-    explicit Grid(const mpi::Comm& comm = mpi::Comm::Self(), int height = 0, GridOrder order = COLUMN_MAJOR)
+    Grid() : Grid(mpi::COMM_WORLD) {}  // Grid.hpp:18 (over COMM_WORLD)
+    explicit Grid(const mpi::Comm& comm, int height = 0, GridOrder order = COLUMN_MAJOR)
         : comm_(comm) {
         elx_grid_t g = nullptr;
         detail::Check(elx_grid_create(&g, comm.Handle(), height, order));
@@ -209,20 +403,62 @@ public:
     const T* LockedBuffer() const noexcept { return buf_; }
     T* Buffer(Int i, Int j) { return Buffer() + i + j * ld_; }
     const T* LockedBuffer(Int i, Int j) const noexcept { return buf_ + i + j * ld_; }
-    // SyncInfoFromMatrix: the HIP stream the matrix's device work is ordered on (null on the CPU)
+    // the HIP stream the matrix's device work is ordered on (null on the CPU);
+    // SyncInfoFromMatrix(M).Stream()
     void* Stream() const noexcept { return stream_; }
+    // SyncInfoFromMatrix(M) as a GPU SyncInfo (null stream and event on the CPU)
+    SyncInfo<Device::GPU> GPUSyncInfo() const noexcept {
+        return SyncInfo<Device::GPU>(static_cast<hipStream_t>(stream_), static_cast<hipEvent_t>(event_));
+    }
 
 protected:
     T* buf_ = nullptr;
     Int h_ = 0, w_ = 0, ld_ = 1;
     bool owned_ = true, locked_ = false;
     void* stream_ = nullptr;
+    void* event_ = nullptr;
 };
+
+namespace detail {
+// MultiSync over local matrices (Gemm.cpp:178-180 MakeMultiSync(C, A, B)): the
+// master's stream waits for the operands' queued work on entry, the operands'
+// streams wait for the master's on exit; nothing on the CPU or on one stream.
+template <typename T>
+class LocalFence {
+public:
+    LocalFence(const AbstractMatrix<T>& master, std::initializer_list<const AbstractMatrix<T>*> others)
+        : gpu_(master.GetDevice() == Device::GPU), m_(master.GPUSyncInfo()) {
+        if (!gpu_) return;
+        for (const AbstractMatrix<T>* o : others)
+            if (o && o->Stream() != master.Stream()) o_.push_back(o->GPUSyncInfo());
+        for (const auto& o : o_) AddSynchronizationPoint(o, m_);
+    }
+    ~LocalFence() {
+        if (gpu_ && !o_.empty()) {
+            AddSynchronizationPoint(m_);
+            for (const auto& o : o_) hydrogen::details::AddSyncPoint(m_, o);
+        }
+    }
+    LocalFence(const LocalFence&) = delete;
+    LocalFence& operator=(const LocalFence&) = delete;
+
+private:
+    bool gpu_;
+    SyncInfo<Device::GPU> m_;
+    std::vector<SyncInfo<Device::GPU>> o_;
+};
+}  // namespace detail
 
 template <typename T, Device D = Device::CPU>
 class Matrix : public AbstractMatrix<T> {
 public:
-    Matrix() { this->stream_ = DefaultStream(); }
+    Matrix() {
+        if (D == Device::GPU) {
+            const SyncInfo<Device::GPU>& si = gpu::DefaultSyncInfo();
+            this->stream_ = si.Stream();
+            this->event_ = si.Event();
+        }
+    }
     Matrix(Int height, Int width, Int ldim = 0) : Matrix() { Resize(height, width, ldim); }
     Matrix(const Matrix& A) : Matrix() { *this = A; }
     Matrix(Matrix&& A) noexcept { Swap(A); }
@@ -230,6 +466,7 @@ public:
     Matrix& operator=(const Matrix& A) {  // deep copy (El::Copy of Matrix)
         if (this == &A) return *this;
         Resize(A.Height(), A.Width());
+        detail::LocalFence<T> fence(*this, {&A});
         detail::Check(elx_matrix_copy(detail::TypeCode<T>::value, static_cast<int>(D), A.Height(), A.Width(),
                                       A.LockedBuffer(), A.LDim(), this->buf_, this->ld_, this->stream_));
         return *this;
@@ -277,15 +514,46 @@ public:
         if (D == Device::GPU) detail::Check(elx_memcpy_h2d(p, &v, sizeof(T), this->stream_));
         else *p = v;
     }
-    // SetSyncInfo(Matrix, SyncInfo): subsequent device work queues on `stream`
-    void SetStream(void* stream) { if (D == Device::GPU) this->stream_ = stream ? stream : DefaultStream(); }
+    // subsequent device work queues on `stream` (null: the default stream),
+    // ordered after the work already queued on the old one
+    void SetStream(void* stream) {
+        if (D != Device::GPU) return;
+        SetSyncInfo(SyncInfo<Device::GPU>(static_cast<hipStream_t>(stream ? stream : gpu::DefaultSyncInfo().Stream()),
+                                          nullptr));
+    }
+    // Matrix<T,Device::GPU>::GetSyncInfo / SetSyncInfo (Matrix/decl.hpp:478-479,
+    // impl_gpu.hpp:503-513): Set merges the non-null parts.  A stream change on a
+    // matrix that owns pool memory first fences the new stream after the old
+    // one, so the buffer's later stream-ordered free (on the new stream) comes
+    // after every use; on the local-block view of a DistMatrix (Matrix()) the
+    // DistMatrix itself moves to the new stream.
+    SyncInfo<D> GetSyncInfo() const noexcept { return SyncInfoOf(this->stream_, this->event_, Tag<D>{}); }
+    void SetSyncInfo(SyncInfo<D> const& si) { SetSyncInfoImpl(si); }
+
+    // DistMatrix::Matrix() binds its local view to the owning DistMatrix
+    void BindOwner_(elx_dm_t owner) { owner_ = owner; }
+    void ViewStream_(void* stream) { if (D == Device::GPU) this->stream_ = stream; }
 
 private:
-    static void* DefaultStream() {
-        if (D != Device::GPU) return nullptr;
-        void* s = nullptr;
-        detail::Check(elx_default_stream(&s));
-        return s;
+    template <Device> struct Tag {};
+    static SyncInfo<Device::CPU> SyncInfoOf(void*, void*, Tag<Device::CPU>) noexcept { return {}; }
+    static SyncInfo<Device::GPU> SyncInfoOf(void* s, void* e, Tag<Device::GPU>) noexcept {
+        return SyncInfo<Device::GPU>(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e));
+    }
+    void SetSyncInfoImpl(SyncInfo<Device::CPU> const&) {}
+    void SetSyncInfoImpl(SyncInfo<Device::GPU> const& si) {
+        SyncInfo<Device::GPU> cur = this->GPUSyncInfo();
+        const hipStream_t old = cur.Stream();
+        cur.Merge(si);
+        if (cur.Stream() != old) {
+            if (owner_) {
+                detail::Check(elx_dm_set_stream(owner_, cur.Stream()));
+            } else if (this->owned_ && this->buf_ && old) {
+                AddSynchronizationPoint(SyncInfo<Device::GPU>(old, cur.Event()), cur);
+            }
+        }
+        this->stream_ = cur.Stream();
+        this->event_ = cur.Event();
     }
     void CheckIndex(Int i, Int j) const {
         if (i < 0 || j < 0 || i >= this->h_ || j >= this->w_) throw LogicError("Entry out of bounds");
@@ -324,10 +592,28 @@ private:
     void Swap(Matrix& o) noexcept {
         std::swap(this->buf_, o.buf_); std::swap(this->h_, o.h_); std::swap(this->w_, o.w_);
         std::swap(this->ld_, o.ld_); std::swap(this->owned_, o.owned_); std::swap(this->locked_, o.locked_);
-        std::swap(this->stream_, o.stream_); std::swap(cap_, o.cap_);
+        std::swap(this->stream_, o.stream_); std::swap(this->event_, o.event_); std::swap(cap_, o.cap_);
+        std::swap(owner_, o.owner_);
     }
     std::size_t cap_ = 0;
+    elx_dm_t owner_ = nullptr;
 };
+
+// SyncInfoFromMatrix / SetSyncInfo (Matrix/decl.hpp:287-296,521-533)
+template <typename T>
+SyncInfo<Device::CPU> SyncInfoFromMatrix(Matrix<T, Device::CPU> const&) {
+    return SyncInfo<Device::CPU>{};
+}
+template <typename T>
+SyncInfo<Device::GPU> SyncInfoFromMatrix(Matrix<T, Device::GPU> const& mat) {
+    return mat.GetSyncInfo();
+}
+template <typename T, Device D>
+void SetSyncInfo(Matrix<T, D>&, SyncInfo<D> const&) {}
+template <typename T>
+void SetSyncInfo(Matrix<T, Device::GPU>& mat, SyncInfo<Device::GPU> const& si) {
+    mat.SetSyncInfo(si);
+}
 
 // ---- DistMatrix ----------------------------------------------------------------
 template <typename T>
@@ -441,10 +727,14 @@ public:
     DistMatrix operator()(Range rows, AllRange) const { return View(rows.beg, rows.end, 0, this->Width()); }
 
 private:
+    // the view keeps its event; its stream is the DistMatrix's, and
+    // SetSyncInfo on it moves the DistMatrix (SyncInfoFromMatrix(A.LockedMatrix())
+    // / SetSyncInfo(A.Matrix(), si), the reference callers' idiom)
     void RefreshLocal() const {
         const Int ld = this->LDim() > 1 ? this->LDim() : 1;
         local_.Attach(this->LocalHeight(), this->LocalWidth(), const_cast<T*>(this->LockedBuffer()), ld);
-        local_.SetStream(this->Stream());
+        local_.ViewStream_(this->Stream());
+        local_.BindOwner_(this->h());
     }
     mutable El::Matrix<T, D> local_;
     DistMatrix(const El::Grid& g, elx_dm_t view) : AbstractDistMatrix<T>(g, U, V, D, view) {}
@@ -466,6 +756,7 @@ void Gemm(Orientation orientA, Orientation orientB, T alpha, const AbstractMatri
     const Int m = orientA == NORMAL ? A.Height() : A.Width(), k = orientA == NORMAL ? A.Width() : A.Height();
     const Int kb = orientB == NORMAL ? B.Height() : B.Width(), n = orientB == NORMAL ? B.Width() : B.Height();
     if (m != C.Height() || n != C.Width() || k != kb) throw LogicError("Nonconformal Gemm");
+    detail::LocalFence<T> fence(C, {&A, &B});
     detail::Check(elx_matrix_gemm(detail::TypeCode<T>::value, static_cast<int>(C.GetDevice()), orientA, orientB, m, n,
                                   k, detail::ToDouble(alpha), A.LockedBuffer(), A.LDim(), B.LockedBuffer(), B.LDim(),
                                   detail::ToDouble(beta), C.Buffer(), C.LDim(), C.Stream()));
@@ -597,6 +888,7 @@ template <typename T, typename S> void Scale(S alpha, AbstractMatrix<T>& A) {
 template <typename T, typename S> void Axpy(S alpha, const AbstractMatrix<T>& X, AbstractMatrix<T>& Y) {
     if (X.GetDevice() != Y.GetDevice()) throw LogicError("Axpy: X and Y must be on the same device");
     if (X.Height() != Y.Height() || X.Width() != Y.Width()) throw LogicError("Nonconformal Axpy");
+    detail::LocalFence<T> fence(Y, {&X});
     detail::Check(elx_matrix_axpy(detail::TypeCode<T>::value, static_cast<int>(Y.GetDevice()), Y.Height(), Y.Width(),
                                   static_cast<double>(alpha), X.LockedBuffer(), X.LDim(), Y.Buffer(), Y.LDim(),
                                   Y.Stream()));
@@ -604,6 +896,7 @@ template <typename T, typename S> void Axpy(S alpha, const AbstractMatrix<T>& X,
 template <typename T> void Copy(const AbstractMatrix<T>& A, AbstractMatrix<T>& B) {
     if (A.GetDevice() != B.GetDevice()) throw LogicError("Copy: cross-device Matrix copies go through DistMatrix");
     B.Resize(A.Height(), A.Width());
+    detail::LocalFence<T> fence(B, {&A});
     detail::Check(elx_matrix_copy(detail::TypeCode<T>::value, static_cast<int>(B.GetDevice()), A.Height(), A.Width(),
                                   A.LockedBuffer(), A.LDim(), B.Buffer(), B.LDim(), B.Stream()));
 }
@@ -660,11 +953,25 @@ void Read(AbstractDistMatrix<T>& A, const std::string& filename, FileFormat form
 }
 
 // ---- environment ------------------------------------------------------------------
+// the algorithmic blocksize stack (include/El/core/environment/decl.hpp:88-94,
+// src/blas_like/blocksizes.cpp:38-72); an empty stack is a LogicError
+inline Int Blocksize() {
+    const Int nb = elx_blocksize();
+    if (nb < 0) throw LogicError(elx_last_error());
+    return nb;
+}
 inline void SetBlocksize(Int nb) { detail::Check(elx_set_blocksize(nb)); }
-inline Int Blocksize() { return elx_blocksize(); }
-inline void Initialize() { InitializeRandom(true, 0); }
-inline void Initialize(int&, char**&) { InitializeRandom(true, 0); }
-inline void Finalize() {}
+inline void PushBlocksizeStack(Int nb) { detail::Check(elx_push_blocksize(nb)); }
+inline void PopBlocksizeStack() { detail::Check(elx_pop_blocksize()); }
+inline void EmptyBlocksizeStack() { detail::Check(elx_empty_blocksize_stack()); }
+// El::Initialize (src/core/environment.cpp:215-330): the world communicator
+// from the launcher's environment (RANK / WORLD_SIZE / LOCAL_RANK /
+// MASTER_ADDR: RCCL, one process per GPU; size 1 without them), blocksize
+// stack {128}, deterministic RNG.  Finalize drops the world and the stack.
+inline void Initialize() { detail::Check(elx_initialize()); }
+inline void Initialize(int&, char**&) { Initialize(); }
+inline void Finalize() { detail::Check(elx_finalize()); }
+inline bool Initialized() { return true; }
 
 }  // namespace El
 

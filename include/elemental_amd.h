@@ -114,6 +114,16 @@ int elx_reserved_cus(int* cus);
 int elx_stream_create(void** stream);
 int elx_stream_destroy(void* stream);
 int elx_stream_synchronize(void* stream);
+/* the event half of SyncInfo<Device::GPU> and the fences built on it
+ * (include/hydrogen/device/gpu/rocm/SyncInfo.hpp:15-81: AddSynchronizationPoint
+ * = record, AddSyncPoint = stream waits on event; ROCm.cpp:58-66 default event).
+ * Events are created with timing disabled, as the reference's. */
+int elx_default_event(void** event);
+int elx_event_create(void** event);
+int elx_event_destroy(void* event);
+int elx_event_record(void* event, void* stream);
+int elx_stream_wait_event(void* stream, void* event);
+int elx_event_synchronize(void* event);
 
 /* ---- device memory pool: replaces the hipCUB CachingDeviceAllocator -----
  * (src/core/imports/cub.cpp:1-75, El::Memory mode 1 include/El/core/Memory/impl.hpp:113-187) */
@@ -268,6 +278,28 @@ int elx_comm_wrap_rccl(elx_comm_t* comm, void* nccl_comm);
 int elx_comm_rank(elx_comm_t comm, int* rank);
 int elx_comm_size(elx_comm_t comm, int* size);
 int elx_comm_destroy(elx_comm_t comm);
+/* El::mpi::COMM_WORLD (include/El/core/imports/mpi.hpp:86): the library's world
+ * communicator, size 1 until elx_initialize() builds one from the launcher's
+ * environment or the caller installs one.  elx_comm_world returns a BORROWED
+ * handle (never pass it to elx_comm_destroy); elx_comm_set_world shares the
+ * given communicator (the caller may destroy its own handle afterwards). */
+int elx_comm_world(elx_comm_t* comm);
+int elx_comm_set_world(elx_comm_t comm);
+/* byte broadcast from rank 0 over TCP (rank 0 listens on `port`): the unique-id
+ * exchange for RCCL worlds started without MPI */
+int elx_rendezvous_bcast(void* data, size_t bytes, int rank, int size, const char* addr, int port,
+                         double timeout_s);
+/* stage watchdog: arms a deadline (seconds > 0) for the named stage and prints
+ * "[elx] stage <name>" to stderr; on overrun, or an asynchronous RCCL error on
+ * an owned communicator, every owned RCCL communicator is aborted and the
+ * process exits with status ELX_WATCHDOG_EXIT naming the stage.  seconds <= 0
+ * disarms. */
+#define ELX_WATCHDOG_EXIT 75
+int elx_watchdog_stage(const char* name, double seconds);
+/* text the watchdog writes to stdout before it exits (NULL / "": nothing), and
+ * the exit status it then uses (ELX_WATCHDOG_EXIT until set) — e.g. a
+ * benchmark's result line already measured when a later, optional stage hangs */
+int elx_watchdog_epitaph(const char* text, int exit_code);
 /* raw typed collectives on device (RCCL) or host (callback) buffers, on `stream` */
 int elx_comm_allgather(elx_comm_t comm, int dtype, const void* send, void* recv,
                        int64_t count, void* stream);
@@ -407,9 +439,22 @@ int elx_symm(int side, int uplo, double alpha, elx_dm_t A, elx_dm_t B, double be
              int conjugate);
 /* A := alpha A on its uplo trapezoid (include/El/blas_like/level1/ScaleTrapezoid.hpp:47-88) */
 int elx_dm_scale_trapezoid(double alpha, int uplo, elx_dm_t A, int64_t offset);
-/* Blocksize stack (src/core/environment.cpp:315: default 128) */
+/* Blocksize stack (src/blas_like/blocksizes.cpp:38-72; environment.cpp:314-315
+ * leaves one entry, 128).  elx_blocksize returns -1 on an empty stack (error
+ * text in elx_last_error). */
 int elx_set_blocksize(int64_t nb);
 int64_t elx_blocksize(void);
+int elx_push_blocksize(int64_t nb);
+int elx_pop_blocksize(void);
+int elx_empty_blocksize_stack(void);
+/* El::Initialize / El::Finalize (src/core/environment.cpp:215-330,337-372):
+ * world communicator from RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR (RCCL,
+ * unique id over elx_rendezvous_bcast on ELX_RENDEZVOUS_PORT, default
+ * MASTER_PORT + 1; size 1 without them), blocksize stack reset to {128}, the
+ * deterministic RNG seeded (21<<16)|rank.  Finalize drops the world and
+ * empties the blocksize stack. */
+int elx_initialize(void);
+int elx_finalize(void);
 /* compute panel: how many communicated panels are fused into one local MFMA
  * update (0 = automatic). Changes only the summation order (normwise tol). */
 int elx_set_compute_panel(int64_t kpanel);

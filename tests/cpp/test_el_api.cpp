@@ -299,6 +299,118 @@ int main() {
     El::SetBlocksize(64);
     EXPECT(El::Blocksize() == 64);
     El::SetBlocksize(128);
+
+    // blocksize stack (environment/decl.hpp:88-94, blocksizes.cpp:38-72)
+    {
+        El::PushBlocksizeStack(32);
+        EXPECT(El::Blocksize() == 32);
+        El::SetBlocksize(48);  // SetBlocksize rewrites the top only
+        EXPECT(El::Blocksize() == 48);
+        El::PopBlocksizeStack();
+        EXPECT(El::Blocksize() == 128);
+        El::EmptyBlocksizeStack();
+        bool threw_b = false;
+        try { (void)El::Blocksize(); } catch (const El::LogicError&) { threw_b = true; }
+        EXPECT(threw_b);
+        El::PushBlocksizeStack(128);
+        EXPECT(El::Blocksize() == 128);
+    }
+
+    // El::mpi::COMM_WORLD (imports/mpi.hpp:86): a grid over it, and Grid()
+    {
+        El::Grid gw(El::mpi::COMM_WORLD);
+        EXPECT(gw.Size() == El::mpi::Size(El::mpi::COMM_WORLD) && gw.Size() == 1);
+        EXPECT(El::mpi::Rank() == 0 && El::mpi::COMM_WORLD.Rank() == 0);
+        El::mpi::Barrier(El::mpi::COMM_WORLD);
+        DM<double> Wm(5, 4, gw);
+        El::Fill(Wm, 1.5);
+        EXPECT(Wm.Get(4, 3) == 1.5);
+    }
+
+    // SyncInfo / SyncInfoFromMatrix / SetSyncInfo / MultiSync
+    // (Matrix/decl.hpp:287-296,478-479,521-533, rocm/SyncInfo.hpp:15-81, MultiSync.hpp:33-78)
+    {
+        El::Matrix<double, kDev> Mx(4, 4);
+        auto si = El::SyncInfoFromMatrix(Mx);
+        El::SetSyncInfo(Mx, si);
+        auto ms = El::MakeMultiSync(si, El::SyncInfoFromMatrix(A.LockedMatrix()));
+        (void)ms;
+        El::Synchronize(si);
+        EXPECT(si == El::SyncInfoFromMatrix(Mx));
+    }
+#ifdef EL_TEST_GPU
+    {
+        using GPU = El::SyncInfo<El::Device::GPU>;
+        const GPU& dflt = El::gpu::DefaultSyncInfo();
+        EXPECT(dflt.Stream() != nullptr && dflt.Event() != nullptr);
+        EXPECT(GPU{} == dflt);
+        GPU si1 = El::CreateNewSyncInfo<El::Device::GPU>();
+        GPU si2 = El::CreateNewSyncInfo<El::Device::GPU>();
+        EXPECT(si1.Stream() && si1.Event() && si1.Stream() != si2.Stream() && si1 != si2);
+        // Merge keeps the parts the argument leaves null
+        GPU part(si1.Stream(), nullptr);
+        GPU merged = dflt;
+        merged.Merge(part);
+        EXPECT(merged.Stream() == si1.Stream() && merged.Event() == dflt.Event());
+
+        // event-fenced hand-off: X is produced on si1 by a ~2 ms GEMM, consumed
+        // on si2 right after; the fence is what makes the consumer see it
+        const Int nn = 4096;
+        El::Matrix<double, El::Device::GPU> P(nn, nn), Q(nn, nn), X(nn, nn), Yh(nn, nn);
+        for (auto* M : {&P, &Q, &X, &Yh}) El::SetSyncInfo(*M, si1);
+        EXPECT(El::SyncInfoFromMatrix(X).Stream() == si1.Stream() && El::SyncInfoFromMatrix(X).Event() == si1.Event());
+        El::Fill(P, 1.0);
+        El::Fill(Q, 0.5);
+        El::Fill(X, -1.0);
+        El::Fill(Yh, -3.0);
+        El::Synchronize(si1);
+        El::Gemm(El::NORMAL, El::NORMAL, 1.0, P, Q, 0.0, X);  // X = 2048 everywhere (exact), on si1
+        El::AddSynchronizationPoint(si1, si2);                // si2 waits for si1's queued work
+        El::SetSyncInfo(Yh, si2);                              // Yh moves to si2 (fenced after si1)
+        {
+            auto fence = El::MakeMultiSync(si2, si1);           // on exit si1 waits for si2
+            El::Copy(X, Yh);                                    // on Yh's stream, si2; X on si1 is fenced in too
+        }
+        El::Synchronize(si1);                                  // si1 now covers si2's copy
+        EXPECT(Yh.Get(0, 0) == 2048.0 && Yh.Get(nn - 1, nn - 1) == 2048.0 && Yh.Get(nn / 2, 17) == 2048.0);
+
+        // local Gemm with A and B on a stream other than C's (Gemm.cpp:178-180
+        // MakeMultiSync(C, A, B)): C on si2 must see P written on si1
+        El::Matrix<double, El::Device::GPU> Cg(64, 64);
+        El::SetSyncInfo(Cg, si2);
+        El::Fill(Cg, 0.0);
+        El::Synchronize(si2);
+        El::Scale(2.0, P);                                    // P = 2 (on si1), queued behind nothing long ...
+        El::Gemm(El::NORMAL, El::NORMAL, 1.0, Q, P, 0.0, X);   // ... then a long GEMM on si1 rewrites X = 4096
+        El::Matrix<double, El::Device::GPU> Xv;
+        Xv.LockedAttach(64, nn, X.LockedBuffer(), X.LDim());   // a view of X's first 64 rows, on si1
+        El::SetSyncInfo(Xv, si1);
+        El::Matrix<double, El::Device::GPU> Pv;
+        Pv.LockedAttach(nn, 64, P.LockedBuffer(), P.LDim());
+        El::SetSyncInfo(Pv, si1);
+        El::Gemm(El::NORMAL, El::NORMAL, 1.0, Xv, Pv, 0.0, Cg); // on si2: Cg = 4096 * 2 * 4096
+        El::Synchronize(si2);
+        EXPECT(Cg.Get(0, 0) == 4096.0 * 2.0 * 4096.0 && Cg.Get(63, 63) == 4096.0 * 2.0 * 4096.0);
+
+        // a DistMatrix's local block: SetSyncInfo on Matrix() moves the DistMatrix
+        DM<double> Ds(6, 5, g);
+        El::SetSyncInfo(Ds.Matrix(), si1);
+        EXPECT(Ds.Stream() == static_cast<void*>(si1.Stream()));
+        EXPECT(El::SyncInfoFromMatrix(Ds.LockedMatrix()).Stream() == si1.Stream());
+        El::Fill(Ds, 4.0);
+        EXPECT(Ds.Get(5, 4) == 4.0);
+        El::SetSyncInfo(Ds.Matrix(), dflt);
+        EXPECT(Ds.Stream() == static_cast<void*>(dflt.Stream()));
+
+        for (auto* M : {&P, &Q, &X, &Yh, &Cg}) El::SetSyncInfo(*M, dflt);
+        El::Synchronize(dflt);
+        El::Synchronize(si1);
+        El::Synchronize(si2);
+        El::DestroySyncInfo(si1);
+        El::DestroySyncInfo(si2);
+        EXPECT(si1.Stream() == nullptr && si1.Event() == nullptr);
+    }
+#endif
     El::Finalize();
     if (failures) {
         std::fprintf(stderr, "%d failures\n", failures);

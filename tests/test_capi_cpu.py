@@ -8,6 +8,7 @@ import shutil
 import subprocess
 
 import numpy as np
+import oracle
 import pytest
 
 from elemental_amd import _lib as L
@@ -86,6 +87,28 @@ def test_cpu_matrices_local_gemm_and_redistribution():
     S = el.DistMatrix(g, el.F64, el.STAR, el.VC, el.CPU)
     S.assign(A)
     assert np.array_equal(S.get_local(), Ah)
+
+
+@pytest.mark.parametrize("dtype", [el.F64, el.F32])
+def test_frobenius_norm_scaled(dtype):
+    """El::FrobeniusNorm with the reference's scaled sum of squares
+    (Frobenius.cpp:37-44): entries whose squares overflow (1e200 in f64, 1e30 in
+    f32) or underflow give the right norm; NaN propagates; zero is zero."""
+    g = el.Grid()
+    big = 1e200 if dtype == el.F64 else 1e30
+    npt = np.float64 if dtype == el.F64 else np.float32
+    for scale in (1.0, big, 1.0 / big):
+        a = (oracle.hash_matrix(13, 7, 5) * scale).astype(npt)
+        A = el.DistMatrix(g, dtype, el.MC, el.MR, el.CPU, height=13, width=7)
+        A.set_local(a)
+        want = scale * np.linalg.norm(oracle.hash_matrix(13, 7, 5))
+        got = el.FrobeniusNorm(A)
+        assert np.isfinite(got) and abs(got - want) <= 1e-5 * want, (scale, got, want)
+    Z = el.DistMatrix(g, dtype, el.MC, el.MR, el.CPU, height=4, width=4)
+    el.Zero(Z)
+    assert el.FrobeniusNorm(Z) == 0.0
+    Z.Set(1, 2, float("nan"))
+    assert np.isnan(el.FrobeniusNorm(Z))
 
 
 def test_cpp_dropin_header_compiles_and_runs(tmp_path):

@@ -1,0 +1,110 @@
+"""Fail-safe multi-rank execution (the stage watchdog), the TCP rendezvous that
+carries the RCCL unique id for El::Initialize, and the environment API the
+drop-in header exposes (COMM_WORLD, the blocksize stack) — all on CPU.
+
+The watchdog replaces the error fencing the reference gets from MPI / Aluminum
+(include/El/core/imports/mpi/aluminum_comm.hpp:174-212): a stage that overruns
+its deadline ends the process with a non-zero status naming the stage, instead
+of leaving a multi-rank job hung."""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "_failsafe_worker.py")
+WATCHDOG_EXIT = 75
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(*args, timeout=60):
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, WORKER, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    return p, time.monotonic() - t0
+
+
+def test_watchdog_ends_an_overrunning_stage():
+    p, dt = _run("deadline", "unit stage", 1.0, 30)
+    assert p.returncode == WATCHDOG_EXIT, (p.returncode, p.stderr)
+    assert "[elx] stage unit stage (deadline 1 s)" in p.stderr
+    assert "FATAL in stage 'unit stage'" in p.stderr and "deadline of 1 s exceeded" in p.stderr
+    assert "survived" not in p.stdout
+    assert dt < 20
+
+
+def test_watchdog_disarmed_stage_runs_to_the_end():
+    p, _ = _run("disarm", 0.5, 1.5)
+    assert p.returncode == 0, p.stderr
+    assert "survived" in p.stdout and "[elx] stage disarmed" in p.stderr
+
+
+def test_watchdog_gloo_world2_peer_never_joins():
+    """Rank 0 blocks inside a 1x2 El::Gemm whose peer never enters it: the
+    watchdog ends rank 0 at its 3 s deadline (stage named), and the straggler at
+    its own — nobody hangs for gloo's 30-minute default."""
+    port = _port()
+    procs = [subprocess.Popen([sys.executable, WORKER, "gloo_hang", str(r), "2", str(port)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    t0 = time.monotonic()
+    outs = [p.communicate(timeout=90) for p in procs]
+    dt = time.monotonic() - t0
+    assert [p.returncode for p in procs] == [WATCHDOG_EXIT, WATCHDOG_EXIT], [o[1][-2000:] for o in outs]
+    assert "FATAL in stage 'c3 timed'" in outs[0][1]
+    assert "FATAL in stage 'straggler'" in outs[1][1]
+    assert "gemm returned" not in outs[0][0]
+    assert dt < 60
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rendezvous_bcast(world):
+    port = _port()
+    procs = [subprocess.Popen([sys.executable, WORKER, "rendezvous", str(r), str(world), str(port)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in reversed(range(world))]
+    outs = [p.communicate(timeout=60) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1] for o in outs]
+    assert sorted(o[0].strip() for o in outs) == [f"rank {r} ok" for r in range(world)]
+
+
+def test_rendezvous_times_out_without_rank0():
+    from elemental_amd import el
+    from elemental_amd import _lib as L
+    with pytest.raises(L.ElxError, match="could not reach rank 0"):
+        el.rendezvous_bcast(None, 16, 1, 2, "127.0.0.1", _port(), 0.5)
+
+
+def test_blocksize_stack_and_comm_world():
+    """PushBlocksizeStack / PopBlocksizeStack / EmptyBlocksizeStack
+    (environment/decl.hpp:88-94) and COMM_WORLD (size 1 without a launcher)."""
+    from elemental_amd import el
+    from elemental_amd import _lib as L
+    el.Initialize()
+    assert el.Blocksize() == 128
+    el.PushBlocksizeStack(64)
+    assert el.Blocksize() == 64
+    el.SetBlocksize(32)
+    assert el.Blocksize() == 32
+    el.PopBlocksizeStack()
+    assert el.Blocksize() == 128
+    el.EmptyBlocksizeStack()
+    with pytest.raises(L.LogicError, match="empty stack"):
+        el.Blocksize()
+    with pytest.raises(L.LogicError, match="empty"):
+        el.PopBlocksizeStack()
+    el.PushBlocksizeStack(128)
+    w = el.Comm.world()
+    assert w.size == 1 and w.rank == 0
+    g = el.Grid(w)
+    assert (g.height, g.width) == (1, 1)
+    el.Finalize()
+    el.PushBlocksizeStack(128)  # Finalize empties the stack; later tests expect the default
+    assert el.Blocksize() == 128

@@ -281,6 +281,66 @@ def test_gpu_rccl_single_rank_redistribution_and_summa():
     _rccl_spawn(W.raw_coll_worker, 1)
 
 
+def _failsafe(*args, env=None, timeout=120):
+    import os
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_failsafe_worker.py")
+    full = dict(os.environ, **(env or {}))
+    return subprocess.run([sys.executable, worker, *map(str, args)], capture_output=True, text=True,
+                          timeout=timeout, env=full)
+
+
+def test_gpu_rccl_watchdog_aborts_overrunning_stage():
+    """World-1 RCCL (init and the four grid splits),
+    a GEMM over it, then a stage that overruns its deadline: the watchdog aborts
+    the RCCL communicators and exits with ELX_WATCHDOG_EXIT naming the stage."""
+    p = _failsafe("rccl_hang", 2.0)
+    assert p.returncode == el.WATCHDOG_EXIT, p.stdout + p.stderr
+    assert "FATAL in stage 'rccl stage'" in p.stderr and "RCCL communicator(s)" in p.stderr
+    assert "aborting 0 RCCL" not in p.stderr
+    assert "survived" not in p.stdout
+
+
+def test_gpu_initialize_rccl_world_from_launcher_env():
+    """El::Initialize under torch.distributed.run's variables builds COMM_WORLD
+    over RCCL (unique id through the TCP rendezvous; size 1 on this box)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = _failsafe("init_env", env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
+                                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "init ok" in p.stdout
+
+
+@pytest.mark.parametrize("hang,code", [("timed", 75), ("cpu_baseline", 0)])
+def test_gpu_bench_stage_hang(hang, code):
+    """bench.py under an injected hang (ELX_BENCH_HANG): in the timed stage the
+    watchdog ends the run non-zero naming the stage and no line is printed;
+    in a stage after the main point the line is still printed, with that stage
+    marked, and the exit status is 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--n", "2048", "--steps", "1",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=200,
+                       env=dict(os.environ, ELX_BENCH_HANG=hang))
+    assert p.returncode == code, p.stdout + p.stderr
+    assert f"FATAL in stage '{hang}'" in p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if code:
+        assert not lines
+    else:
+        assert len(lines) == 1
+        rec = json.loads(lines[0])
+        assert rec["value"] > 0 and rec["verify"]["ok"] and "error" in rec[hang]
+
+
 @pytest.mark.skipif(el.device_count() < 2, reason="needs >= 2 GPUs (one RCCL rank per GPU)")
 @pytest.mark.parametrize("world,height", [(2, 1), (2, 2)])
 def test_gpu_rccl_multi_gpu(world, height):
