@@ -803,19 +803,29 @@ def raw_coll_worker(rank: int, world: int, port: int):
 
 
 # tests/golden/mkl_summa.npz cases: dtype_grid_nb_mxnxk
+# tests/golden/mkl_summa_orient.npz: NT / TN / TT through SUMMA_C, TN / NN through SUMMA_DOT
+MKL_ORIENT = [f"{t}_{g}_{o}_C" for t in ("f64", "f32")
+              for g in ("2x2_nb16_45x37x61", "2x4_nb16_53x66x130") for o in ("NT", "TN", "TT")] + \
+             [f"{t}_{g}_{o}_DOT" for t in ("f64", "f32")
+              for g in ("2x2_nb16_20x24x130", "2x4_nb16_19x30x257") for o in ("TN", "NN")]
+MKL_C1 = ["f64_2x2_nb128_4096x4096x4096_NN_C_sample"]
 MKL_SUMMA = ["f64_2x2_nb16_45x37x61", "f64_1x2_nb8_30x41x27", "f64_2x4_nb16_53x66x130", "f64_2x2_nb128_260x200x300",
              "f32_2x2_nb16_45x37x61", "f32_1x2_nb8_30x41x27", "f32_2x4_nb16_53x66x130", "f32_2x2_nb128_260x200x300"]
 
 
-def mkl_summa_worker(rank: int, world: int, port: int, height: int, device: int, keys):
-    """El::Gemm(NN, GEMM_SUMMA_C) with the fixture's Blocksize on its grid,
-    against the reference's SUMMA_NNC evaluated through MKL rank by rank
-    (tests/golden/mkl_summa.npz, tools/make_mkl_golden.py): each rank checks
-    its own local block with the north_star normwise bound (global norms)."""
+def mkl_summa_worker(rank: int, world: int, port: int, height: int, device: int, keys,
+                     fixture: str = "mkl_summa.npz"):
+    """El::Gemm with the fixture's orientation, algorithm and Blocksize on its
+    grid, against the reference's SUMMA evaluated through MKL rank by rank
+    (tests/golden/mkl_summa*.npz, tools/make_mkl_golden.py): each rank checks
+    its own local block with the north_star normwise bound (global norms).
+    Keys: {f64,f32}_{r}x{c}_nb{nb}_{m}x{n}x{k}[_{oA}{oB}_{C,DOT}[_sample]]; a
+    _sample fixture holds rows 0::sr x columns 0::sc of the result and only
+    those entries are compared."""
     import oracle
     el, comm = init(rank, world, port)
     try:
-        gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_summa.npz"))
+        gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", fixture))
         for key in keys:
             parts = key.split("_")
             r, c = map(int, parts[1].split("x"))
@@ -823,27 +833,44 @@ def mkl_summa_worker(rank: int, world: int, port: int, height: int, device: int,
                 continue
             nb = int(parts[2][2:])
             m, n, k = map(int, parts[3].split("x"))
+            oa, ob = (parts[4][0], parts[4][1]) if len(parts) > 4 else ("N", "N")
+            alg = {"C": el.GEMM_SUMMA_C, "DOT": el.GEMM_SUMMA_DOT}[parts[5]] if len(parts) > 5 else el.GEMM_SUMMA_C
+            sample = parts[-1] == "sample"
             dt = np.float64 if parts[0] == "f64" else np.float32
             dtype = el.F64 if dt == np.float64 else el.F32
             s = [int(x) for x in gold[key + "_seed"]]
-            Ag = oracle.hash_matrix(m, k, s[0], 0.0, 0.1, dt)
-            Bg = oracle.hash_matrix(k, n, s[1], 0.0, 0.1, dt)
+            ah, aw = (m, k) if oa == "N" else (k, m)
+            bh, bw = (k, n) if ob == "N" else (n, k)
+            Ag = oracle.hash_matrix(ah, aw, s[0], 0.0, 0.1, dt)
+            Bg = oracle.hash_matrix(bh, bw, s[1], 0.0, 0.1, dt)
             Cg = oracle.hash_matrix(m, n, s[2], 0.0, 0.1, dt)
             g = el.Grid(comm, r)
             assert (g.height, g.width) == (r, c)
             el.SetBlocksize(nb)
-            A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=k)
-            B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=k, width=n)
+            A = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=ah, width=aw)
+            B = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=bh, width=bw)
             C = el.DistMatrix(g, dtype, el.MC, el.MR, device, height=m, width=n)
             A.set_local(oracle.local_block(Ag, el.MC, el.MR, r, c, g.vc_rank))
             B.set_local(oracle.local_block(Bg, el.MC, el.MR, r, c, g.vc_rank))
             C.set_local(oracle.local_block(Cg, el.MC, el.MR, r, c, g.vc_rank))
-            el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C, el.GEMM_SUMMA_C)
+            orient = {"N": el.NORMAL, "T": el.TRANSPOSE}
+            el.Gemm(orient[oa], orient[ob], 0.5, A, B, -0.5, C, alg)
             got = C.get_local().astype(np.float64)
-            want = oracle.local_block(gold[key], el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
-            num = np.linalg.norm(got - want) if got.size else 0.0
             den = np.linalg.norm(Ag.astype(np.float64)) * np.linalg.norm(Bg.astype(np.float64)) * k * np.finfo(dt).eps
+            if sample:
+                sr, sc = (int(x) for x in gold[key + "_stride"])
+                mc, mr = g.vc_rank % r, g.vc_rank // r
+                rows = np.arange(mc, m, r)   # this rank's global rows / columns ([MC,MR], alignment 0)
+                cols = np.arange(mr, n, c)
+                ri, ci = np.nonzero(rows % sr == 0)[0], np.nonzero(cols % sc == 0)[0]
+                got = got[np.ix_(ri, ci)]
+                want = gold[key][np.ix_(rows[ri] // sr, cols[ci] // sc)].astype(np.float64)
+            else:
+                want = oracle.local_block(gold[key], el.MC, el.MR, r, c, g.vc_rank).astype(np.float64)
+            num = np.linalg.norm(got - want) if got.size else 0.0
             assert np.isfinite(got).all() and num <= 10 * den, f"{key} rank {rank}: {num / den:.3g}"
+            if sample:  # the sampled entries are checked one by one as well
+                assert np.all(np.abs(got - want) <= 64 * np.finfo(dt).eps * k * 0.01), f"{key} rank {rank}"
         el.SetBlocksize(128)
         finish()
     except Exception:

@@ -68,7 +68,8 @@ def rccl_hang(seconds: float):
     comm = el.Comm.rccl(0, 1, uid)
     grid = el.Grid(comm, 1)
     A = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=256, width=256).fill_hash(1, 0.0, 1.0)
-    el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, A, 0.0, A.like())
+    C = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=256, width=256)
+    el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, A, 0.0, C)
     el.device_synchronize()
     el.watchdog_stage("rccl stage", seconds)
     time.sleep(60)
@@ -85,7 +86,7 @@ def init_env():
     assert w.size == 1 and w.rank == 0
     grid = el.Grid(w)
     A = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=64, width=64).fill_hash(1, 0.0, 1.0)
-    C = A.like()
+    C = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=64, width=64)
     el.Gemm(el.NORMAL, el.NORMAL, 1.0, A, A, 0.0, C)
     a = A.get_local()
     assert np.allclose(C.get_local(), a @ a, rtol=1e-12, atol=1e-12)

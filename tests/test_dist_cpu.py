@@ -172,3 +172,12 @@ def test_summa_matches_mkl_reference_path(world):
     path's own arithmetic: SUMMA_NNC evaluated rank by rank through MKL
     2021.4.0 (tests/golden/mkl_summa.npz), 1x2 / 2x2 / 2x4 grids, f64 and f32."""
     _spawn(W.mkl_summa_worker, world, 2 if world > 2 else 1, el.CPU, W.MKL_SUMMA)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_summa_orientations_match_mkl_reference_path(world):
+    """NT / TN / TT through SUMMA_C and TN / NN through SUMMA_DOT on 2x2 and 2x4
+    (Device::CPU over gloo) against the reference's loops evaluated rank by rank
+    through MKL (tests/golden/mkl_summa_orient.npz; TN.hpp:252-291,371-416,
+    NT.hpp:251-294, TT.hpp:195-240, NN.hpp:461-511)."""
+    _spawn(W.mkl_summa_worker, world, 2, el.CPU, W.MKL_ORIENT, "mkl_summa_orient.npz")

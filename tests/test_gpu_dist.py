@@ -258,6 +258,16 @@ def test_gpu_summa_matches_mkl_reference_path(world):
     reference CPU path's SUMMA_NNC evaluated through MKL rank by rank
     (tests/golden/mkl_summa.npz): 1x2 / 2x2 / 2x4, f64 and f32, north_star bound."""
     _spawn(W.mkl_summa_worker, world, 2 if world > 2 else 1, el.GPU, W.MKL_SUMMA)
+    if world > 2:
+        _spawn(W.mkl_summa_worker, world, 2, el.GPU, W.MKL_ORIENT, "mkl_summa_orient.npz")
+
+
+def test_gpu_summa_matches_mkl_at_c1_size():
+    """C1 at its own size (El::Gemm NN f64 4096^3 on a 2x2 grid, Blocksize 128)
+    on the GPU path (MFMA updates, host-staged panels) against the reference's
+    SUMMA_NNC through MKL rank by rank: a 111 x 100 sample of the result
+    (tests/golden/mkl_summa_orient.npz), normwise and entrywise."""
+    _spawn(W.mkl_summa_worker, 4, 2, el.GPU, W.MKL_C1, "mkl_summa_orient.npz")
 
 
 def _rccl_spawn(fn, world, *args):

@@ -218,6 +218,35 @@ def test_oracle_matches_mkl_local_gemm():
     assert worst < 1, worst
 
 
+def test_oracle_matches_mkl_summa_orientations():
+    """The oracle's plain GEMM (any summation order is inside the bound) against
+    the reference's SUMMA_C for NT / TN / TT and SUMMA_DOT for TN / NN evaluated
+    rank by rank through MKL, and C1's sampled 4096^3 result against the
+    oracle's simulated SUMMA_NNC at the sampled entries."""
+    d = np.load(os.path.join(GOLD, "mkl_summa_orient.npz"))
+    keys = [k for k in d.files if k != "_mkl" and not k.endswith(("_seed", "_stride"))]
+    assert len(keys) == 21
+    for key in keys:
+        parts = key.split("_")
+        dt = np.float64 if parts[0] == "f64" else np.float32
+        m, n, k = map(int, parts[3].split("x"))
+        ta, tb = parts[4][0], parts[4][1]
+        s = [int(x) for x in d[key + "_seed"]]
+        A = oracle.hash_matrix(m if ta == "N" else k, k if ta == "N" else m, s[0], 0.0, 0.1, dt)
+        B = oracle.hash_matrix(k if tb == "N" else n, n if tb == "N" else k, s[1], 0.0, 0.1, dt)
+        C = oracle.hash_matrix(m, n, s[2], 0.0, 0.1, dt)
+        eps = np.finfo(dt).eps
+        if parts[-1] == "sample":
+            sr, sc = (int(x) for x in d[key + "_stride"])
+            # the sampled rows of A and columns of B give the sampled entries exactly
+            ref = 0.5 * (A[::sr, :].astype(np.float64) @ B[:, ::sc].astype(np.float64)) - 0.5 * C[::sr, ::sc]
+            err = np.abs(ref - d[key])
+            assert err.max() <= 1e-14, key
+            continue
+        ref = oracle.gemm(ta, tb, 0.5, A, B, -0.5, C)
+        assert oracle.parity_ratio(ref, d[key], A, B, k, eps) < 0.5, key
+
+
 def test_oracle_matches_mkl_summa():
     """The oracle's simulated SUMMA_NNC and its plain GEMM against the
     reference's SUMMA_NNC evaluated rank by rank through MKL (Scale(beta, C),

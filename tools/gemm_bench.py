@@ -2,7 +2,8 @@
 
   python tools/gemm_bench.py [dt,ta,tb,m,n,k ...] [--vendor]
 
-Random Uniform(-0.5, 0.5) operands (column-major), beta = 1.  --vendor also
+Random Uniform(-0.5, 0.5) operands (column-major), beta = 1; each timing is the best
+of 3 runs of back-to-back calls (launch latency amortised).  --vendor also
 times torch.matmul (hipBLASLt) on the same shape as a reference point.
 """
 import os
@@ -20,16 +21,25 @@ DEFAULT = ["f64,0,0,16384,16384,16384", "f64,0,0,32768,16384,4096", "f32,0,0,163
 
 
 def timeit(go, reps):
+    """Best of `reps` timings of `inner` back-to-back calls (inner sized to fill
+    ~30 ms, so launch and sync latency do not count for small shapes); returns
+    seconds per call."""
     go()
     torch.cuda.synchronize()
     L.call("elx_device_synchronize")
+    t = time.perf_counter()
+    go()
+    L.call("elx_device_synchronize")
+    torch.cuda.synchronize()
+    inner = max(1, min(200, int(0.03 / max(time.perf_counter() - t, 1e-6))))
     best = 1e30
     for _ in range(reps):
         t = time.perf_counter()
-        go()
+        for _ in range(inner):
+            go()
         L.call("elx_device_synchronize")
         torch.cuda.synchronize()
-        best = min(best, time.perf_counter() - t)
+        best = min(best, (time.perf_counter() - t) / inner)
     return best
 
 
