@@ -86,6 +86,29 @@ def test_local_gemm_known_answer_exact(k):
     assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * A @ B - C)
 
 
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+@pytest.mark.parametrize("shape", [(2048, 2048, 2072), (2000, 1990, 1056), (1024, 1024, 288)])
+def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
+    """Grids of at most one workgroup per CU take the 32-deep-slab fp64 kernel
+    (gemm_f64g.hip, Shape<128,64,32>), an odd 16 through the 16-deep kernel and
+    the k % 16 tail through the general one (2072 = 2048 + 16 + 8): integer
+    operands, so every orientation must match exactly."""
+    m, n, k = shape
+    rng = np.random.default_rng(k)
+    A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
+    B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(np.float64))
+    C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(np.float64))
+    dA, dB, dC = dev(A), dev(B), dev(C)
+    torch.cuda.synchronize()
+    L.call("elx_gemm_f64", OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0],
+           -1.0, dC.data_ptr(), m, None)
+    sync()
+    opA = A if ta == "N" else A.T
+    opB = B if tb == "N" else B.T
+    assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * (opA @ opB) - C)
+
+
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
