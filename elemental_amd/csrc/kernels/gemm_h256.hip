@@ -636,6 +636,257 @@ __global__ __launch_bounds__(NT, 1) void gemm_h4d_kernel(H2Params p) {
     epilogue<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
+// ---------------------------------------------------------------------------
+// Four-wave kernel: the same 256 x 256 output tile, but 4 waves (2 x 2), one per
+// SIMD, each owning 128 x 128 = 8 x 8 accumulators (256 AGPRs; the wave has the
+// whole 512-entry file).  Per FLOP this halves the B-fragment LDS reads of the
+// eight-wave kernels (a wave's fragments feed 8 x 8 MFMAs instead of 8 x 4), cuts
+// a third of all LDS instructions, and leaves no partner wave on the SIMD to take
+// matrix-pipe slots or issue bandwidth (MI355X_MICROARCH.md "Two waves per SIMD"
+// items 1-3): each wave issues its own fragment reads and staging between its
+// MFMAs.  hipBLASLt's bf16 kernels on these shapes have the same geometry
+// (MT256x256x64, MI16x16, 4 waves: profiles/r03_vendor_pmc.json).
+//
+// Staging unit = one operand's K-tile image (256 rows x 64 k = 32 KiB, the KC /
+// RC half images of the kernels above: 128-B KC rows, 256-B RC k-rows), in a
+// ring of 5 slots (160 KiB): A_t is unit 2t, B_t unit 2t+1, unit u in slot u % 5.
+// Each K-tile runs as two k-steps of 64 MFMAs per wave:
+//   (t,0): MFMAs on fragments (t,0) [set X]; read fragments (t,1) [set Y] from
+//          A_t, B_t; stage A_{t+2} into B_{t-1}'s slot; then vmcnt(8) (A_{t+1}
+//          and B_{t+1} landed, A_{t+2} may stay in flight), lgkmcnt(0), barrier;
+//   (t,1): MFMAs on (t,1) [Y]; read (t+1,0) [X] from A_{t+1}, B_{t+1}; stage
+//          B_{t+2} into A_t's slot; lgkmcnt(0), no barrier.
+// RAW: A_{t+1}, B_{t+1} are read from (t,1) on, after every wave's wait and the
+// barrier ending (t,0).  WAR: A_t's and B_t's last reads are issued in (t,0) and
+// retired before that barrier; their slots are restaged in (t,1) and (t+1,0).
+// No wave can be two k-steps ahead of another (it would have passed a barrier
+// the other has not reached), so one barrier per K-tile suffices.  Units past
+// the end re-stage the last K-tile into a slot nobody reads again, so every
+// k-step issues the same 8 pieces and the counted wait is exact without branches.
+// The accumulators are tied to AGPRs through inline asm (mfma_acc).
+// ---------------------------------------------------------------------------
+namespace w4 {
+constexpr int UNIT = 256 * BK * 2;  // one operand's K-tile image: 32 KiB
+constexpr int NSLOT = 5;
+
+// per-lane offset (elements from the image's corner at k0) of piece j (0..31)
+// of one operand's K-tile image: half j >> 4, wave-instruction j & 15 of it, as
+// stage_half lays them out
+template <bool KC>
+__device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld) {
+    const int h = j >> 4, ins = j & 15;
+    if (KC) {
+        const int r = ins * 8 + (l >> 3);
+        const int c = (l & 7) ^ swz_kc(r);
+        const i64 row0 = h * 128 + r;
+        const i64 row = R0 + row0 < rows ? row0 : rows - 1 - R0;
+        return row * ld + 8 * c;
+    } else {
+        const int kk = ins * 4 + (l >> 4);
+        const int c = (l & 15) ^ swz_rc(kk);
+        const i64 col0 = h * 128 + 8 * c;
+        const i64 col = R0 + col0 <= rows - 8 ? col0 : rows - 8 - R0;
+        return col + kk * ld;
+    }
+}
+
+template <bool KC>
+__device__ __forceinline__ const uint16_t* tile_base(const uint16_t* X, i64 ld, i64 R0, i64 k0) {
+    return KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
+}
+
+template <bool BUF, bool KC>
+__device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int j,
+                                      lds_char* img) {
+    if constexpr (BUF) {
+        const BufferSrc<uint16_t> src(tile_base<KC>(X, ld, R0, k0), (KC ? 256 : BK) * ld * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + j * 1024), 16,
+                                                 off, 0, 0, 0);
+    } else {
+        glds16(tile_base<KC>(X, ld, R0, k0) + goff, img + j * 1024);
+    }
+}
+
+struct Sets {
+    u32x4 a[8], b[8];
+};
+
+// acc += a b with the accumulator tied to one AGPR quad.  Written as asm: the
+// builtin's accumulators get rotated through fresh registers (earlyclobber form)
+// at 256 live accumulators, costing ~2 v_accvgpr moves per MFMA.  Only other
+// MFMAs of the same accumulator read it inside the loop (accumulate chains need
+// no wait states); the kernel pads before the epilogue's first read (settle).
+template <bool BF16>
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const u32x4& a, const u32x4& b) {
+    if constexpr (BF16) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// 8-pass MFMA result -> any non-MFMA reader: 12 wait states (then the registers
+// are handed to the compiler through empty asm statements ordered after the pad)
+__device__ __forceinline__ void settle(f32x4 (&acc)[8][8]) {
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+}
+
+// C tile of one wave (128 x 128): accumulator (mi, ni) holds rows
+// rb + 16 mi + 4 (l >> 4) + {0..3}, column cb + 16 ni + (l & 15).  One row of
+// accumulators at a time (C loads, then stores), so at most 32 values live in
+// VGPRs; interior tiles with an 8-B-aligned C take the unchecked path.
+template <bool BF16>
+__device__ __forceinline__ void epilogue4(const H2Params& p, const f32x4 (&acc)[8][8], i64 m0, i64 n0, int wr, int wc,
+                                          int l) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 128 + (l & 15);
+    const bool fast = p.vec_c && m0 + BM <= p.m && n0 + BN <= p.n;
+    if (fast) {
+        uint16_t* o0 = p.C + rb + cb * p.ldc;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            uint2 cv[8];
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                cv[ni] = p.beta != 0.f ? *reinterpret_cast<const uint2*>(o0 + mi * 16 + ni * 16 * p.ldc) : make_uint2(0, 0);
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) {
+                const uint16_t in[4] = {(uint16_t)(cv[ni].x & 0xffff), (uint16_t)(cv[ni].x >> 16),
+                                        (uint16_t)(cv[ni].y & 0xffff), (uint16_t)(cv[ni].y >> 16)};
+                uint16_t r16[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = p.alpha * acc[mi][ni][r];
+                    if (p.beta != 0.f) v += p.beta * E::load(in[r]);
+                    r16[r] = E::store(v);
+                }
+                *reinterpret_cast<uint2*>(o0 + mi * 16 + ni * 16 * p.ldc) =
+                    make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16), (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+            }
+        }
+    } else {
+        epilogue<BF16, 8>(p, acc, m0, n0, wr, wc, l);
+    }
+}
+
+struct Pieces {  // this wave's staging pieces w + 4u, u = 0..7, of each operand's image
+    int offA[8], offB[8];
+    i64 gA[8], gB[8];
+};
+
+// One k-step: 64 MFMAs on `cur`, the 16 fragments of k-step `srd` of the K-tile in
+// (rdA, rdB) into `nxt`, and the 8 pieces of one unit (operand SB ? B : A at k0)
+// into `st`.  The LDS pointers are __restrict__ so the inlined accesses carry
+// alias scopes: hipcc's waitcnt pass then knows the in-flight DMA cannot alias
+// the fragment reads (without them it drains vmcnt(0) before every
+// ds_read_b64_tr_b16).
+template <bool BF16, bool KCA, bool KCB, bool BUF, bool SB, int FL, int WP>
+__device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
+                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
+                                      f32x4 (&acc)[8][8], const Sets& cur, Sets& nxt) {
+    // Staging placement: B_{t+2} (SB, k-step (t,1)) has the shorter lead (its slot
+    // frees at the barrier before this k-step, its data is read after the next
+    // one), so its 8 pieces go out in the first half of the k-step, one per
+    // 4-MFMA group; A_{t+2} (k-step (t,0)) in the second half.  Wave WP issues
+    // after MFMA WP of the group, so the four waves' pieces do not queue behind
+    // each other in the CU's texture path.
+    constexpr int QB = SB ? 0 : 8;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int mi = q >> 1, ni = (q & 1) * 4 + t;
+            mfma_acc<BF16>(acc[mi][ni], cur.a[mi], cur.b[ni]);
+            if (!(FL & 1) && t == WP && q >= QB && q < QB + 8) {
+                const int u = q - QB;
+                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+            }
+        }
+        if (FL & 2) {
+        } else if (q < 8) nxt.a[q] = frag<KCA>(rdA + wr * HALF, q * 16, srd, l);
+        else nxt.b[q - 8] = frag<KCB>(rdB + wc * HALF, (q - 8) * 16, srd, l);
+    }
+}
+}  // namespace w4
+
+// FL: timing ablations only (wrong results): 1 = no staging after the prologue,
+// 2 = no fragment reads, 4 = no barrier
+template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
+__global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
+    using namespace w4;
+    __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
+    lds_char* lds = (lds_char*)lds_raw;
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+
+    Pieces pc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.offA[u] = (int)(pc.gA[u] * 2);
+        pc.offB[u] = (int)(pc.gB[u] * 2);
+    }
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    auto kt = [&](int t) { return (i64)min(t, nt - 1) * BK; };
+    auto slot = [&](int u) { return lds + (u % NSLOT) * UNIT; };
+    // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; fragments (0,0)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar8();
+    Sets X, Y;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        X.a[q] = frag<KCA>(lds + wr * HALF, q * 16, 0, l);
+        X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    auto loop = [&](auto wp) {
+        constexpr int WP = decltype(wp)::value;
+        for (int t = 0; t < nt; ++t) {
+            // (t,0): stage A_{t+2} into B_{t-1}'s slot
+            w4::kstep<BF16, KCA, KCB, BUF, false, FL, WP>(p, m0, n0, w, l, wr, wc, pc, slot(2 * t), slot(2 * t + 1), 1,
+                                                         slot(2 * t + 4), kt(t + 2), acc, X, Y);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (!(FL & 4)) bar8();
+            // (t,1): stage B_{t+2} into A_t's slot
+            w4::kstep<BF16, KCA, KCB, BUF, true, FL, WP>(p, m0, n0, w, l, wr, wc, pc, slot(2 * t + 2), slot(2 * t + 3),
+                                                        0, slot(2 * t + 5), kt(t + 2), acc, Y, X);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    };
+    if (w == 0) loop(std::integral_constant<int, 0>{});
+    else if (w == 1) loop(std::integral_constant<int, 1>{});
+    else if (w == 2) loop(std::integral_constant<int, 2>{});
+    else loop(std::integral_constant<int, 3>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
+    w4::settle(acc);
+    w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
+}
+
 // One 16 x 16 accumulator tile: rows i..i+15 (4 per lane), column j.
 template <bool BF16>
 __device__ __forceinline__ void epi_one(const H2Params& p, const f32x4 v4, i64 i, i64 j) {
@@ -714,6 +965,22 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
     // kernel on NN / TN / NT, C5 32768^3 1340 -> 1414 TF; profiles/r02_h16_deep.log)
     static const bool balanced = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 'b'; }();
     static const bool deep = [] { const char* v = getenv("ELX_H16_KERNEL"); return !v || v[0] == 'd'; }();
+    // =w: the four-wave kernel (ELX_H16_FLAGS picks its timing ablations)
+    static const bool four = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 'w'; }();
+    if (four) {
+        const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
+        auto go = [&](auto kernel) {
+            hipLaunchKernelGGL(kernel, dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+            return hipGetLastError();
+        };
+        if constexpr (BF16 && KCB) {
+            if (buf && fl == 1) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 1>);
+            if (buf && fl == 2) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2>);
+            if (buf && fl == 4) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 4>);
+            if (buf && fl == 3) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 3>);
+        }
+        return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
+    }
     if (deep && fl == 0) {
         if (dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2))
             return launch(gemm_h4d_kernel<BF16, KCA, KCB, true>, p, s);
@@ -748,6 +1015,7 @@ int GroupM() {
 
 }  // namespace
 
+#ifndef ELX_KERNEL_PROBE
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
     const bool kca = ta, kcb = !tb;
@@ -776,6 +1044,8 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
     return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);
 }
+
+#endif  // ELX_KERNEL_PROBE
 
 }  // namespace kern
 }  // namespace elx

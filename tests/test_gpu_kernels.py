@@ -146,6 +146,41 @@ def test_local_gemm_16bit(kind, ta, tb, shape):
         assert np.linalg.norm(gotf - exact) <= np.linalg.norm(refh - exact) + 1e-3
 
 
+@pytest.mark.parametrize("kind", ["f16", "bf16"])
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+@pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640)])
+def test_local_gemm_16bit_exact(kind, ta, tb, shape):
+    """Integer operands in [-2, 2]: every partial sum is exact in the f32
+    accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
+    to 16 bits, and the result must equal numpy's rounding of the exact value bit
+    for bit.  k = 2112: 66 slabs of 32 (the 16-bit kernels' main loop over many
+    wraps of their LDS ring); 2312 columns: ragged edge tiles.  (k a multiple of
+    64: a k tail is a second pass that adds to the already rounded C.)"""
+    m, n, k = shape
+    rng = np.random.default_rng(m + n + k)
+    A = rng.integers(-2, 3, (m, k) if ta == "N" else (k, m)).astype(np.float32)
+    B = rng.integers(-2, 3, (k, n) if tb == "N" else (n, k)).astype(np.float32)
+    C = rng.integers(-64, 65, (m, n)).astype(np.float32)
+    opA = A if ta == "N" else A.T
+    opB = B if tb == "N" else B.T
+    exact = 1.0 * (opA.astype(np.float64) @ opB.astype(np.float64)) - 2.0 * C
+    if kind == "f16":
+        enc = lambda x: np.asfortranarray(x.astype(np.float16))
+        fn, want = L.lib().elx_gemm_f16, exact.astype(np.float16).view(np.uint16)
+    else:
+        enc = lambda x: np.asfortranarray(oracle.f32_to_bf16_bits(x))
+        fn, want = L.lib().elx_gemm_bf16, oracle.f32_to_bf16_bits(exact.astype(np.float32))
+    dA, dB, dC = dev(enc(A)), dev(enc(B)), dev(enc(C))
+    torch.cuda.synchronize()
+    L.check(fn(OPS[ta], OPS[tb], m, n, k, 1.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0], -2.0,
+               dC.data_ptr(), m, None))
+    sync()
+    got = host(dC, (m, n), np.uint16)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
+
+
 DTYPES = [(L.F64, np.float64), (L.F32, np.float32), (L.F16, np.float16), (L.BF16, "bf16")]
 
 

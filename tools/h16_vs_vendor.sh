@@ -1,12 +1,12 @@
 #!/bin/bash
 # Side-by-side counters of our 16-bit GEMM kernel and hipBLASLt's on one shape:
-#   tools/h16_vs_vendor.sh <tag> <dt> <n> <ta> <tb>
+#   [IMPLS="ours vendor"] tools/h16_vs_vendor.sh <tag> <dt> <n> <ta> <tb>
 # kernel-trace stats, then separate PMC passes (clock/MFMA/LDS, FETCH_SIZE, L2 hit).
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
 mkdir -p $R/gpurun_out
-for impl in ours vendor; do
+for impl in ${IMPLS:-ours vendor}; do
   V=""; [ $impl = vendor ] && V="--vendor"
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_${impl}_trace -o t -- python3 $R/tools/prof_gemm.py "$@" 10 $V > $R/gpurun_out/${TAG}_${impl}_trace.log 2>&1
   rc=$?; echo "$impl trace rc=$rc"; case $rc in 124|137|134|139) exit $rc;; esac
