@@ -781,7 +781,7 @@ struct Pieces {  // this wave's staging pieces w + 4u, u = 0..7, of each operand
 // alias scopes: hipcc's waitcnt pass then knows the in-flight DMA cannot alias
 // the fragment reads (without them it drains vmcnt(0) before every
 // ds_read_b64_tr_b16).
-template <bool BF16, bool KCA, bool KCB, bool BUF, bool SB, int FL, int WP>
+template <bool BF16, bool KCA, bool KCB, bool BUF, bool SB, int FL>
 __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
                                       const Pieces& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
@@ -789,31 +789,33 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
     // Staging placement: B_{t+2} (SB, k-step (t,1)) has the shorter lead (its slot
     // frees at the barrier before this k-step, its data is read after the next
     // one), so its 8 pieces go out in the first half of the k-step, one per
-    // 4-MFMA group; A_{t+2} (k-step (t,0)) in the second half.  Wave WP issues
-    // after MFMA WP of the group, so the four waves' pieces do not queue behind
-    // each other in the CU's texture path.
-    constexpr int QB = SB ? 0 : 8;
+    // 4-MFMA group; A_{t+2} (k-step (t,0)) in the second half.  The 16 fragment
+    // reads go out in the first half, two per group, so they have retired long
+    // before the lgkmcnt(0) that ends the k-step.
+    constexpr int QB = SB && !(FL & 64) ? 0 : 8;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int mi = q >> 1, ni = (q & 1) * 4 + t;
             mfma_acc<BF16>(acc[mi][ni], cur.a[mi], cur.b[ni]);
-            if (!(FL & 1) && t == WP && q >= QB && q < QB + 8) {
+            if (!(FL & 1) && t == 1 && q >= QB && q < QB + 8) {
                 const int u = q - QB;
                 if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
                 else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
             }
         }
-        if (FL & 2) {
-        } else if (q < 8) nxt.a[q] = frag<KCA>(rdA + wr * HALF, q * 16, srd, l);
-        else nxt.b[q - 8] = frag<KCB>(rdB + wc * HALF, (q - 8) * 16, srd, l);
+        if (!(FL & 2) && q < 8) {
+            nxt.a[q] = frag<KCA>(rdA + wr * HALF, q * 16, srd, l);
+            nxt.b[q] = frag<KCB>(rdB + wc * HALF, q * 16, srd, l);
+        }
     }
 }
 }  // namespace w4
 
 // FL: timing ablations only (wrong results): 1 = no staging after the prologue,
-// 2 = no fragment reads, 4 = no barrier
+// 2 = no fragment reads, 4 = no barrier, 32 = no wait for the staged K-tile;
+// variant (correct): 64 = B_{t+2}'s pieces in the second half of k-step (t,1)
 template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
@@ -863,25 +865,31 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    auto loop = [&](auto wp) {
-        constexpr int WP = decltype(wp)::value;
-        for (int t = 0; t < nt; ++t) {
-            // (t,0): stage A_{t+2} into B_{t-1}'s slot
-            w4::kstep<BF16, KCA, KCB, BUF, false, FL, WP>(p, m0, n0, w, l, wr, wc, pc, slot(2 * t), slot(2 * t + 1), 1,
-                                                         slot(2 * t + 4), kt(t + 2), acc, X, Y);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if constexpr (!(FL & 4)) bar8();
-            // (t,1): stage B_{t+2} into A_t's slot
-            w4::kstep<BF16, KCA, KCB, BUF, true, FL, WP>(p, m0, n0, w, l, wr, wc, pc, slot(2 * t + 2), slot(2 * t + 3),
-                                                        0, slot(2 * t + 5), kt(t + 2), acc, Y, X);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
+    // One K-tile; J = t % 5 makes every slot a compile-time offset of the LDS
+    // base (the loop is unrolled by the ring length), so the fragment reads and
+    // the DMA destinations need no address arithmetic in the loop.
+    auto ktile = [&](auto jc, int t) {
+        constexpr int J = decltype(jc)::value;
+        constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
+                      sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
+        // (t,0): stage A_{t+2} into B_{t-1}'s slot
+        w4::kstep<BF16, KCA, KCB, BUF, false, FL>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
+                                                 lds + st0 * UNIT, kt(t + 2), acc, X, Y);
+        if constexpr (!(FL & 32)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(FL & 4)) bar8();
+        // (t,1): stage B_{t+2} into A_t's slot
+        w4::kstep<BF16, KCA, KCB, BUF, true, FL>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+                                                lds + st1 * UNIT, kt(t + 2), acc, Y, X);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    if (w == 0) loop(std::integral_constant<int, 0>{});
-    else if (w == 1) loop(std::integral_constant<int, 1>{});
-    else if (w == 2) loop(std::integral_constant<int, 2>{});
-    else loop(std::integral_constant<int, 3>{});
+    for (int t = 0; t < nt; t += NSLOT) {
+        ktile(std::integral_constant<int, 0>{}, t);
+        if (t + 1 < nt) ktile(std::integral_constant<int, 1>{}, t + 1);
+        if (t + 2 < nt) ktile(std::integral_constant<int, 2>{}, t + 2);
+        if (t + 3 < nt) ktile(std::integral_constant<int, 3>{}, t + 3);
+        if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
     w4::settle(acc);
     w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
@@ -976,8 +984,9 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
         if constexpr (BF16 && KCB) {
             if (buf && fl == 1) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 1>);
             if (buf && fl == 2) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2>);
-            if (buf && fl == 4) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 4>);
             if (buf && fl == 3) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 3>);
+            if (buf && fl == 64) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 64>);
+            if (buf && fl == 96) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 96>);
         }
         return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
     }
