@@ -37,13 +37,22 @@ constexpr int BN = 128, BK = 16, GROUP_M = 8;
 // Tile shapes: BM = 128 (two workgroups per CU) or 256 (one workgroup per CU,
 // 25 % fewer staged bytes per FLOP); wave tiles WTM x 64 with WTM = 32 (2 x 4
 // accumulators, 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read
-// per MFMA, half the waves).
-template <int BM_, int WTM_ = 32>
+// per MFMA, half the waves).  Slab depth SK = 16 (two 32-KiB stages: two
+// workgroups per CU) or 32 (two 64-KiB stages: one workgroup per CU, for grids
+// that have at most one workgroup per CU anyway: twice the MFMAs between
+// barriers, half the barriers and DMA waits).
+template <int BM_, int WTM_ = 32, int SK_ = BK>
 struct Shape {
-    static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW;
-    static constexpr int IMGA = BM * BK * 8, IMGB = BN * BK * 8, STAGE = IMGA + IMGB;
-    static constexpr int WAVES_PER_EU = NW * (BM_ == 128 ? 2 : 1) / 4;  // waves resident per SIMD
+    static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW, SK = SK_;
+    static constexpr int IMGA = BM * SK * 8, IMGB = BN * SK * 8, STAGE = IMGA + IMGB;
+    static constexpr int WAVES_PER_EU = NW * (BM_ == 128 && SK_ == 16 ? 2 : 1) / 4;  // waves resident per SIMD
 };
+
+// KC images: rows of SK doubles (128 B at SK 16, 256 B at SK 32); 16-B chunk c of
+// row r stored at c ^ swz_kc(r): at SK 16 (r>>1)&7, at SK 32 r&15 (the 32 lanes of
+// a ds_read_b64 half-wave read 16 rows x one chunk: 16 distinct chunks, 256 B).
+template <int SK>
+__device__ __forceinline__ int swz_kc(int r) { return SK == 16 ? (r >> 1) & 7 : r & 15; }
 
 struct GParams {
     i64 m, n, k;  // k: multiple of BK
@@ -72,19 +81,20 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
     tn = inner / gsz;
 }
 
-// Stage one operand image (ROWS operand rows from global row R, 16 k from k0):
-// ROWS/8 wave-instructions of 1 KiB dealt over NW waves.
-template <bool BUF, bool KC, int ROWS, int NW>
+// Stage one operand image (ROWS operand rows from global row R, SK k from k0):
+// ROWS*SK/128 wave-instructions of 1 KiB dealt over NW waves.
+template <bool BUF, bool KC, int ROWS, int NW, int SK>
 __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
-    constexpr int NINS = ROWS * BK * 8 / 1024;
-    const DmaSrc<BUF, double> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? ROWS : BK) * ld * 8);
+    constexpr int NINS = ROWS * SK * 8 / 1024;
+    constexpr int CPR = SK / 2, RPI = 64 / CPR;  // 16-B chunks per row, rows per instruction
+    const DmaSrc<BUF, double> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? ROWS : SK) * ld * 8);
 #pragma unroll
     for (int q = 0; q < NINS / NW; ++q) {
         const int ins = w + NW * q;
-        if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
-            const int r = ins * 8 + (l >> 3);
-            const int c = (l & 7) ^ ((r >> 1) & 7);
+        if (KC) {  // X(row, k) = X[k + row*ld]; RPI rows of SK*8 B per instruction
+            const int r = ins * RPI + l / CPR;
+            const int c = (l % CPR) ^ swz_kc<SK>(r);
             const i64 row = R + r < rows ? r : rows - 1 - R;  // rows past the edge: any valid data
             src.load(row * ld + 2 * c, img + ins * 1024);
         } else {   // X(row, k) = X[row + k*ld]; k-rows of ROWS*8 B, 1 KiB per instruction
@@ -98,11 +108,11 @@ __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64
 }
 
 // Operand of one 16x16x4 MFMA: lane l holds X(R0 + (l&15), 4s + (l>>4)).
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int SK>
 __device__ __forceinline__ double opnd(const lds_char* img, int R0, int s, int l) {
     const int r = R0 + (l & 15), k = 4 * s + (l >> 4);
     int off;
-    if (KC) off = r * 128 + ((((k >> 1) ^ ((r >> 1) & 7))) << 4) + ((k & 1) << 3);
+    if (KC) off = r * (SK * 8) + ((((k >> 1) ^ swz_kc<SK>(r))) << 4) + ((k & 1) << 3);
     else off = k * (ROWS * 8) + ((((r >> 1) ^ ((k & 1) << 3))) << 4) + ((r & 1) << 3);
     return *(const __attribute__((address_space(3))) double*)(img + off);
 }
@@ -120,18 +130,18 @@ template <typename SH, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
                                      const lds_char* __restrict__ cur, f64x4 (&acc)[SH::MI][4]) {
     if (more) {
-        stage_img<BUF, KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<BUF, KCB, BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
+        stage_img<BUF, KCA, SH::BM, SH::NW, SH::SK>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<BUF, KCB, BN, SH::NW, SH::SK>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
     }
     const lds_char* Ai = cur;
     const lds_char* Bi = cur + SH::IMGA;
 #pragma unroll
-    for (int s = 0; s < BK / 4; ++s) {
+    for (int s = 0; s < SH::SK / 4; ++s) {
         double a[SH::MI], b[4];
 #pragma unroll
-        for (int mi = 0; mi < SH::MI; ++mi) a[mi] = opnd<KCA, SH::BM>(Ai, f.wr * SH::WTM + mi * 16, s, f.l);
+        for (int mi = 0; mi < SH::MI; ++mi) a[mi] = opnd<KCA, SH::BM, SH::SK>(Ai, f.wr * SH::WTM + mi * 16, s, f.l);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB, BN>(Bi, f.wc * 64 + ni * 16, s, f.l);
+        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB, BN, SH::SK>(Bi, f.wc * 64 + ni * 16, s, f.l);
 #pragma unroll
         for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
@@ -172,9 +182,9 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
-    const int nt = (int)(p.k / BK);
-    stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
+    const int nt = (int)(p.k / SH::SK);
+    stage_img<BUF, KCA, BM, SH::NW, SH::SK>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<BUF, KCB, BN, SH::NW, SH::SK>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (FL & 4) {
@@ -182,7 +192,8 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     }
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * SH::SK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE,
+                                lds + cur * STAGE, acc);
         if (FL & 8) {  // raw barrier: no vmcnt drain (ablation only)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
@@ -260,7 +271,7 @@ hipError_t launch_g(GParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
     static const bool global_only = [] { const char* v = getenv("ELX_F64G_STAGE"); return v && v[0] == 'g'; }();
-    if (!global_only && dma_fits(KCA ? SH::BM : BK, p.lda, 8) && dma_fits(KCB ? BN : BK, p.ldb, 8))
+    if (!global_only && dma_fits(KCA ? SH::BM : SH::SK, p.lda, 8) && dma_fits(KCB ? BN : SH::SK, p.ldb, 8))
         return launch_b<SH, KCA, KCB, true>(p, grid, s);
     return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
@@ -295,6 +306,24 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (!ta && tb) ? 32 : 64;
+    // ELX_F64G_DEEP=1: grids of at most one workgroup per CU (no split-k) take the
+    // 32-deep slabs on the first kmain/32*32 of k, an odd 16 through the 16-deep
+    // kernel (beta = 1).  Off by default: 2048^3 NN 53.8 vs 60.6 TF with the
+    // 16-deep kernel at one workgroup per CU (profiles/r03_f64_small.log).
+    static const bool deep_few = [] { const char* v = getenv("ELX_F64G_DEEP"); return v && v[0] == '1'; }();
+    const i64 tiles = (i64)((m + 127) / 128) * p.tiles_n;
+    if (deep_few && bm == 128 && kchunk == kmain && tiles <= 256 && kmain >= 32) {
+        GParams q = p;
+        q.k = q.kchunk = kmain / 32 * 32;
+        hipError_t e = wtm == 64 ? launch_shape<Shape<128, 64, 32>>(ta, !tb, q, s) : launch_shape<Shape<128, 32, 32>>(ta, !tb, q, s);
+        if (e != hipSuccess || q.k == kmain) return e;
+        q.A = ta ? A + q.k : A + q.k * lda;
+        q.B = tb ? B + q.k * ldb : B + q.k;
+        q.k = q.kchunk = kmain - q.k;
+        q.alpha = alpha;
+        q.beta = 1.0;
+        return wtm == 64 ? launch_shape<Shape<128, 64>>(ta, !tb, q, s) : launch_shape<Shape<128>>(ta, !tb, q, s);
+    }
     if (bm == 256) return wtm == 64 ? launch_shape<Shape<256, 64>>(ta, !tb, p, s) : launch_shape<Shape<256>>(ta, !tb, p, s);
     if (wtm == 64) return launch_shape<Shape<128, 64>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);

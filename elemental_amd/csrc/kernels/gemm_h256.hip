@@ -786,13 +786,15 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
                                       const Pieces& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
                                       f32x4 (&acc)[8][8], const Sets& cur, Sets& nxt) {
-    // Staging placement: B_{t+2} (SB, k-step (t,1)) has the shorter lead (its slot
-    // frees at the barrier before this k-step, its data is read after the next
-    // one), so its 8 pieces go out in the first half of the k-step, one per
-    // 4-MFMA group; A_{t+2} (k-step (t,0)) in the second half.  The 16 fragment
-    // reads go out in the first half, two per group, so they have retired long
-    // before the lgkmcnt(0) that ends the k-step.
-    constexpr int QB = SB && !(FL & 64) ? 0 : 8;
+    // Placement (measured, profiles/r03_h16_four_wave.log): the 16 fragment reads
+    // of the next k-step go out in the first part of the k-step and the 8 staging
+    // pieces in the second half, one per 4-MFMA group, in both k-steps: a piece
+    // issued among the reads costs more MFMA time than the later landing of B_{t+2}
+    // (issued in the second half of (t,1), read after (t+1,0)) costs in waiting.
+    // Default: reads 2 per group in groups 0-7.  Variants: FL 128 = reads 1 per
+    // MFMA in groups 0-3; FL 256 = with 128, pieces in groups 5-12.
+    constexpr int QB = (FL & 256) ? 5 : 8;
+    constexpr int RPG = (FL & 128) ? 4 : 2;  // fragment reads per 4-MFMA group
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #pragma unroll
@@ -804,8 +806,15 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
                 if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
                 else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
             }
+            if constexpr (RPG == 4) {  // read f = 4q + t: A fragments 0-7, then B 0-7
+                const int f = 4 * q + t;
+                if (!(FL & 2) && f < 16) {
+                    if (f < 8) nxt.a[f] = frag<KCA>(rdA + wr * HALF, f * 16, srd, l);
+                    else nxt.b[f - 8] = frag<KCB>(rdB + wc * HALF, (f - 8) * 16, srd, l);
+                }
+            }
         }
-        if (!(FL & 2) && q < 8) {
+        if (RPG == 2 && !(FL & 2) && q < 8) {
             nxt.a[q] = frag<KCA>(rdA + wr * HALF, q * 16, srd, l);
             nxt.b[q] = frag<KCB>(rdB + wc * HALF, q * 16, srd, l);
         }
@@ -815,7 +824,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 
 // FL: timing ablations only (wrong results): 1 = no staging after the prologue,
 // 2 = no fragment reads, 4 = no barrier, 32 = no wait for the staged K-tile;
-// variant (correct): 64 = B_{t+2}'s pieces in the second half of k-step (t,1)
+// placement variants (correct): 128, 384 (kstep)
 template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
@@ -964,17 +973,20 @@ hipError_t launch_p(const H2Params& p, hipStream_t s, int fl) {
 // two-stage bf16 NN or phased bf16 TN kernel.
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h256(const H2Params& p, hipStream_t s) {
-    static const int fl = [] { const char* v = getenv("ELX_H16_FLAGS"); return v ? atoi(v) : 0; }();
-    static const bool two_stage = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 's'; }();
+    // read per call (not cached) so tools/h16_ab.py can interleave kernel variants
+    // in one process (cdna_hip_programming.md §5.4 rule 24); getenv is ~0.1 us
+    const char* kv = getenv("ELX_H16_KERNEL");
+    const char* fv = getenv("ELX_H16_FLAGS");
+    const int fl = fv ? atoi(fv) : 0;
+    const bool two_stage = kv && kv[0] == 's';
     // ELX_H16_KERNEL=b: the balanced-read kernel (+2-5 % over the phased kernel at
     // 16384^3, profiles/r02_h16_experiments.log); =p the phased kernel (and its
-    // ablations), =s the two-stage kernel
+    // ablations), =s the two-stage kernel, =w the four-wave kernel
     // default: the deep-prefetch two-phase kernel (+2-5 % over the balanced-read
     // kernel on NN / TN / NT, C5 32768^3 1340 -> 1414 TF; profiles/r02_h16_deep.log)
-    static const bool balanced = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 'b'; }();
-    static const bool deep = [] { const char* v = getenv("ELX_H16_KERNEL"); return !v || v[0] == 'd'; }();
-    // =w: the four-wave kernel (ELX_H16_FLAGS picks its timing ablations)
-    static const bool four = [] { const char* v = getenv("ELX_H16_KERNEL"); return v && v[0] == 'w'; }();
+    const bool balanced = kv && kv[0] == 'b';
+    const bool deep = !kv || kv[0] == 'd';
+    const bool four = kv && kv[0] == 'w';
     if (four) {
         const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
         auto go = [&](auto kernel) {
@@ -985,8 +997,8 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
             if (buf && fl == 1) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 1>);
             if (buf && fl == 2) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2>);
             if (buf && fl == 3) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 3>);
-            if (buf && fl == 64) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 64>);
-            if (buf && fl == 96) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 96>);
+            if (buf && fl == 128) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 128>);
+            if (buf && fl == 384) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 384>);
         }
         return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
     }
@@ -1017,9 +1029,9 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-int GroupM() {
-    static const int g = [] { const char* v = getenv("ELX_H16_GROUP"); return v ? atoi(v) : GROUP_M; }();
-    return g;
+int GroupM() {  // per call, like the kernel knobs (tools/h16_ab.py)
+    const char* v = getenv("ELX_H16_GROUP");
+    return v ? atoi(v) : GROUP_M;
 }
 
 }  // namespace
