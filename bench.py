@@ -44,7 +44,7 @@ PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3, "bf16": 2500.0, "f16": 2500.0}
 HBM_PEAK_GBS = 8000.0
 METRIC = "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak"
 KERNEL = {"f64": "gemm_f64g_kernel (LDS-DMA)", "f32": "gemm_f32g_kernel (LDS-DMA)",
-          "bf16": "gemm_h4d_kernel<bf16>", "f16": "gemm_h4d_kernel<f16>"}
+          "bf16": "gemm_h4w_kernel<bf16> (four-wave)", "f16": "gemm_h4w_kernel<f16> (four-wave)"}
 
 
 _WATCHDOG = None  # elemental_amd.el once imported

@@ -791,10 +791,10 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
     // pieces in the second half, one per 4-MFMA group, in both k-steps: a piece
     // issued among the reads costs more MFMA time than the later landing of B_{t+2}
     // (issued in the second half of (t,1), read after (t+1,0)) costs in waiting.
-    // Default: reads 2 per group in groups 0-7.  Variants: FL 128 = reads 1 per
-    // MFMA in groups 0-3; FL 256 = with 128, pieces in groups 5-12.
+    // Default: reads 1 per MFMA in groups 0-3 (+1-2 % over 2 per group in groups
+    // 0-7, FL 128); FL 256: pieces in groups 5-12.
     constexpr int QB = (FL & 256) ? 5 : 8;
-    constexpr int RPG = (FL & 128) ? 4 : 2;  // fragment reads per 4-MFMA group
+    constexpr int RPG = (FL & 128) ? 2 : 4;  // fragment reads per 4-MFMA group
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #pragma unroll
@@ -824,7 +824,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 
 // FL: timing ablations only (wrong results): 1 = no staging after the prologue,
 // 2 = no fragment reads, 4 = no barrier, 32 = no wait for the staged K-tile;
-// placement variants (correct): 128, 384 (kstep)
+// placement variants (correct): 128, 256 (kstep)
 template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
@@ -967,8 +967,8 @@ hipError_t launch_p(const H2Params& p, hipStream_t s, int fl) {
     return launch(gemm_h8p_kernel<BF16, KCA, KCB, BUF>, p, s);
 }
 
-// Kernel choice (launch_h256): deep-prefetch two-phase (default, =d), balanced-read (=b),
-// phased (=p), two-stage (=s);
+// Kernel choice (launch_h256): four-wave (default, =w), deep-prefetch two-phase
+// (=d), balanced-read (=b), phased (=p), two-stage (=s);
 // ELX_H16_FLAGS picks a timing ablation (profiles/r01_h16_ablation.log) of the
 // two-stage bf16 NN or phased bf16 TN kernel.
 template <bool BF16, bool KCA, bool KCB>
@@ -979,14 +979,15 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
     const char* fv = getenv("ELX_H16_FLAGS");
     const int fl = fv ? atoi(fv) : 0;
     const bool two_stage = kv && kv[0] == 's';
-    // ELX_H16_KERNEL=b: the balanced-read kernel (+2-5 % over the phased kernel at
-    // 16384^3, profiles/r02_h16_experiments.log); =p the phased kernel (and its
-    // ablations), =s the two-stage kernel, =w the four-wave kernel
-    // default: the deep-prefetch two-phase kernel (+2-5 % over the balanced-read
-    // kernel on NN / TN / NT, C5 32768^3 1340 -> 1414 TF; profiles/r02_h16_deep.log)
+    // default (=w): the four-wave kernel (+1-3 % over the deep-prefetch kernel on
+    // NN / TN / NT / TT at 16384^3 and 32768^3, profiles/r03_h16_four_wave.log);
+    // =d the deep-prefetch two-phase kernel (+2-5 % over the balanced-read kernel,
+    // profiles/r02_h16_deep.log); =b the balanced-read kernel
+    // (profiles/r02_h16_experiments.log); =p the phased kernel (and its
+    // ablations); =s the two-stage kernel
     const bool balanced = kv && kv[0] == 'b';
-    const bool deep = !kv || kv[0] == 'd';
-    const bool four = kv && kv[0] == 'w';
+    const bool deep = kv && kv[0] == 'd';
+    const bool four = !kv || kv[0] == 'w';
     if (four) {
         const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
         auto go = [&](auto kernel) {
@@ -998,7 +999,7 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
             if (buf && fl == 2) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2>);
             if (buf && fl == 3) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 3>);
             if (buf && fl == 128) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 128>);
-            if (buf && fl == 384) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 384>);
+            if (buf && fl == 256) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 256>);
         }
         return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
     }
@@ -1029,9 +1030,18 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-int GroupM() {  // per call, like the kernel knobs (tools/h16_ab.py)
+bool four_wave() {
+    const char* v = getenv("ELX_H16_KERNEL");
+    return !v || v[0] == 'w';
+}
+
+// Tile-order group height (per call, like the kernel knobs: tools/h16_ab.py).
+// Default 8 for the eight-wave kernels; 4 for the four-wave kernel, whose 32
+// concurrent tiles per XCD then span 4 x 8 tiles (+1-3 % over 8 x 4 at 32768^3
+// and 16384^3, profiles/r03_h16_four_wave.log).
+int GroupM(bool four) {
     const char* v = getenv("ELX_H16_GROUP");
-    return v ? atoi(v) : GROUP_M;
+    return v ? atoi(v) : four ? 4 : GROUP_M;
 }
 
 }  // namespace
@@ -1050,7 +1060,7 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                     ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 64 && m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM()};
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(four_wave())};
     hipError_t e;
     if (is_bf16) {
         if (kca) e = kcb ? launch_h256<true, true, true>(p, s) : launch_h256<true, true, false>(p, s);
