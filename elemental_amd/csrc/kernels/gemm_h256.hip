@@ -803,8 +803,14 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
             mfma_acc<BF16>(acc[mi][ni], cur.a[mi], cur.b[ni]);
             if (!(FL & 1) && t == 1 && q >= QB && q < QB + 8) {
                 const int u = q - QB;
+                if constexpr ((FL & 2048) != 0) {
+                    if (u == 0) __builtin_amdgcn_s_setprio(3);
+                }
                 if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
                 else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+                if constexpr ((FL & 2048) != 0) {
+                    if (u == 7) __builtin_amdgcn_s_setprio(0);
+                }
             }
             if constexpr (RPG == 4) {  // read f = 4q + t: A fragments 0-7, then B 0-7
                 const int f = 4 * q + t;
@@ -824,7 +830,8 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 
 // FL: timing ablations only (wrong results): 1 = no staging after the prologue,
 // 2 = no fragment reads, 4 = no barrier, 32 = no wait for the staged K-tile;
-// placement variants (correct): 128, 256 (kstep)
+// placement variants (correct): 128, 256 (kstep); 2048 = s_setprio 3 over the
+// staging pieces of each k-step (hipBLASLt's loop raises the priority there)
 template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
@@ -1000,6 +1007,8 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
             if (buf && fl == 3) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 3>);
             if (buf && fl == 128) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 128>);
             if (buf && fl == 256) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 256>);
+            if (buf && fl == 2048) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2048>);
+            if (buf && fl == 2304) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2304>);
         }
         return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
     }

@@ -13,10 +13,18 @@ os.makedirs(prof, exist_ok=True)
 stats = glob.glob(os.path.join(out, f"prof_{tag}", "*kernel_stats.csv"))
 if stats:
     shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+# the dominant kernel: the instantiation matching kpat with the largest total time
+# (other instantiations, e.g. the bench's residual-check GEMMs, are excluded:
+# averaging their small dispatches in would dilute every per-launch counter)
+exact = None
+if stats:
+    cand = [r for r in csv.DictReader(open(stats[0])) if kpat in r["Name"]]
+    if cand:
+        exact = max(cand, key=lambda r: float(r["TotalDurationNs"]))["Name"]
 res = {"kernel": None, "counters": {}}
 for d in sorted(glob.glob(os.path.join(out, f"prof_{tag}_pmc*"))):
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
-        rows = [r for r in csv.DictReader(open(f)) if kpat in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(f)) if (r["Kernel_Name"] == exact if exact else kpat in r["Kernel_Name"])]
         if not rows:
             continue
         res["kernel"] = rows[0]["Kernel_Name"]
@@ -40,7 +48,7 @@ if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
     cycles = c["GRBM_GUI_ACTIVE"] / 8.0
     res["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cycles)
     if stats:
-        rows = [r for r in csv.DictReader(open(stats[0])) if kpat in r["Name"]]
+        rows = [r for r in csv.DictReader(open(stats[0])) if (r["Name"] == exact if exact else kpat in r["Name"])]
         if rows:
             secs = float(rows[0]["AverageNs"]) * 1e-9
             res["effective_clock_ghz"] = cycles / secs / 1e9
