@@ -298,7 +298,11 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
 // into kchunk pieces over gridDim.y); the caller adds the k tail.
 hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, double alpha, const double* A,
                             i64 lda, const double* B, i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
-    static const int gm = [] { const char* v = getenv("ELX_F64G_GROUP"); return v ? atoi(v) : GROUP_M; }();
+    static const int gm = [] {  // >= 1: tile_of divides by it
+        const char* v = getenv("ELX_F64G_GROUP");
+        const int g = v ? atoi(v) : GROUP_M;
+        return g >= 1 ? g : 1;
+    }();
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
     GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), kchunk, m * n, gm, rm};
     static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();

@@ -1049,8 +1049,12 @@ bool four_wave() {
 // concurrent tiles per XCD then span 4 x 8 tiles (+1-3 % over 8 x 4 at 32768^3
 // and 16384^3, profiles/r03_h16_four_wave.log).
 int GroupM(bool four) {
+    // clamped to >= 1: tile_of divides by it, and a zero group height ("", "0")
+    // would map workgroups to tiles far outside the operands (an illegal-address
+    // fault, which is how tools/h16_ab.py's "KERNEL:FLAGS" specs once passed 0)
     const char* v = getenv("ELX_H16_GROUP");
-    return v ? atoi(v) : four ? 4 : GROUP_M;
+    const int g = v ? atoi(v) : four ? 4 : GROUP_M;
+    return g >= 1 ? g : 1;
 }
 
 }  // namespace

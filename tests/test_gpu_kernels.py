@@ -181,6 +181,27 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape):
     assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
+def test_local_gemm_16bit_group_knob_clamped(monkeypatch):
+    """ELX_H16_GROUP (the tile-order group height, read per call) of 0 or garbage
+    must not reach the kernel's tile mapping, which divides by it: a zero height
+    once sent workgroups to tiles far outside the operands (an illegal-address
+    fault).  The library clamps it to >= 1; the product is unchanged."""
+    m, n, k = 2048, 2048, 256  # 64 tiles of 256 x 256: the large-tile kernels
+    rng = np.random.default_rng(5)
+    A = rng.integers(-2, 3, (m, k)).astype(np.float32)
+    B = rng.integers(-2, 3, (k, n)).astype(np.float32)
+    want = oracle.f32_to_bf16_bits((A.astype(np.float64) @ B).astype(np.float32))
+    for g in ("0", "", "-3", "1"):
+        monkeypatch.setenv("ELX_H16_GROUP", g)
+        dA, dB = dev(np.asfortranarray(oracle.f32_to_bf16_bits(A))), dev(np.asfortranarray(oracle.f32_to_bf16_bits(B)))
+        dC = dev(np.zeros((m, n), np.uint16))
+        torch.cuda.synchronize()
+        L.check(L.lib().elx_gemm_bf16(0, 0, m, n, k, 1.0, dA.data_ptr(), m, dB.data_ptr(), k, 0.0, dC.data_ptr(), m,
+                                      None))
+        sync()
+        assert np.array_equal(host(dC, (m, n), np.uint16), want), g
+
+
 DTYPES = [(L.F64, np.float64), (L.F32, np.float32), (L.F16, np.float16), (L.BF16, "bf16")]
 
 

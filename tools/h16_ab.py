@@ -35,8 +35,12 @@ def main():
     vs = []
     for v in variants.split(","):
         name, spec = v.split("=")
-        kern, fl, grp = (spec.split(":") + ["0", "8"])[:3]
-        vs.append((name, kern, fl or "0", grp or "8"))
+        parts = spec.split(":")
+        kern = parts[0]
+        fl = parts[1] if len(parts) > 1 and parts[1] else "0"
+        grp = parts[2] if len(parts) > 2 and parts[2] else ""   # "" = the library's default
+        assert grp == "" or int(grp) >= 1, f"group height must be >= 1: {v}"
+        vs.append((name, kern, fl, grp))
     for spec in shapes or ["bf16,1,0,16384,16384,16384"]:
         dt, ta, tb, m, n, k = spec.split(",")
         ta, tb, m, n, k = int(ta), int(tb), int(m), int(n), int(k)
@@ -51,7 +55,11 @@ def main():
         res = {v[0]: [] for v in vs}
         for r in range(rounds):
             for name, kern, fl, grp in vs:
-                os.environ["ELX_H16_KERNEL"], os.environ["ELX_H16_FLAGS"], os.environ["ELX_H16_GROUP"] = kern, fl, grp
+                os.environ["ELX_H16_KERNEL"], os.environ["ELX_H16_FLAGS"] = kern, fl
+                if grp:
+                    os.environ["ELX_H16_GROUP"] = grp
+                else:
+                    os.environ.pop("ELX_H16_GROUP", None)
                 if r == 0:
                     t0 = time.perf_counter()
                     while time.perf_counter() - t0 < 0.5:
