@@ -62,7 +62,7 @@ static double now(void) {
 static int64_t len(int64_t n, int64_t shift, int64_t stride) { return n > shift ? (n - shift - 1) / stride + 1 : 0; }
 
 struct Rank {
-    int rank, n, nb, r, c, mc, mr, world;
+    int rank, n, nb, r, c, mc, mr, world, threads;
     int64_t lh, lw;
     double *A, *B, *C0, *C, *A1, *B1;
     double* slots;
@@ -91,26 +91,37 @@ static void one_step(struct Rank* R) {
         double* s = slot(R, set, R->rank);
         const int64_t ja = (k0 - mr + c - 1) / c, jb = (k0 + kb - mr + c - 1) / c;
         const int64_t ia = (k0 - mc + r - 1) / r, ib = (k0 + kb - mc + r - 1) / r;
-        memcpy(s, R->A + ja * lh, sizeof(double) * lh * (jb - ja));
+        /* the copies run on the rank's threads (the MKL GNU-threading pool's runtime),
+           as a threaded MPI pack would; column by column, so no two threads share a
+           destination cache line of any size that matters */
         double* sb = s + lh * ((nb + c - 1) / c);
-        for (int64_t jl = 0; jl < lw; ++jl) memcpy(sb + jl * (ib - ia), R->B + ia + jl * len(n, mc, r), sizeof(double) * (ib - ia));
+        const int64_t nja = jb - ja, nib = ib - ia, lhB = len(n, mc, r);
+#pragma omp parallel num_threads(R->threads)
+        {
+#pragma omp for schedule(static) nowait
+            for (int64_t q = 0; q < nja; ++q) memcpy(s + q * lh, R->A + (ja + q) * lh, sizeof(double) * lh);
+#pragma omp for schedule(static)
+            for (int64_t jl = 0; jl < lw; ++jl) memcpy(sb + jl * nib, R->B + ia + jl * lhB, sizeof(double) * nib);
+        }
         pthread_barrier_wait(&R->sh->bar);
-        /* receiver copy: column q of A1 is global column k0 + q, held by grid column (k0 + q) mod c */
-        for (int pc = 0; pc < c; ++pc) {
-            const double* pa = slot(R, set, mc + r * pc);
-            const int64_t pja = (k0 - pc + c - 1) / c;
+        /* receiver copy: column q of A1 is global column k0 + q, held by grid column (k0 + q) mod c;
+           row q of B1 is global row k0 + q, held by grid row (k0 + q) mod r */
+#pragma omp parallel num_threads(R->threads)
+        {
+#pragma omp for schedule(static) nowait
             for (int q = 0; q < kb; ++q) {
-                const int j = k0 + q;
-                if (j % c != pc) continue;
+                const int j = k0 + q, pc = j % c;
+                const double* pa = slot(R, set, mc + r * pc);
+                const int64_t pja = (k0 - pc + c - 1) / c;
                 memcpy(R->A1 + (int64_t)q * lh, pa + (j / c - pja) * lh, sizeof(double) * lh);
             }
-        }
-        /* row q of B1 is global row k0 + q, held by grid row (k0 + q) mod r */
-        for (int pr = 0; pr < r; ++pr) {
-            const double* pb = slot(R, set, pr + r * mr) + len(n, pr, r) * ((nb + c - 1) / c);
-            const int64_t pia = (k0 - pr + r - 1) / r, cnt = (k0 + kb - pr + r - 1) / r - pia;
+#pragma omp for schedule(static)
             for (int64_t jl = 0; jl < lw; ++jl)
-                for (int64_t t = 0; t < cnt; ++t) R->B1[(pr + (pia + t) * r - k0) + jl * nb] = pb[t + jl * cnt];
+                for (int pr = 0; pr < r; ++pr) {
+                    const double* pb = slot(R, set, pr + r * mr) + len(n, pr, r) * ((nb + c - 1) / c);
+                    const int64_t pia = (k0 - pr + r - 1) / r, cnt = (k0 + kb - pr + r - 1) / r - pia;
+                    for (int64_t t = 0; t < cnt; ++t) R->B1[(pr + (pia + t) * r - k0) + jl * nb] = pb[t + jl * cnt];
+                }
         }
         const double t1 = now();
         const int ikb = kb;
@@ -124,7 +135,7 @@ static void one_step(struct Rank* R) {
 static int run_rank(int rank, int n, int nb, int r, int c, int threads, double seconds, const char* mkl_path,
                     struct Shared* sh, double* slots, size_t slot_elems) {
     struct Rank R = {0};
-    R.rank = rank; R.n = n; R.nb = nb; R.r = r; R.c = c; R.world = r * c;
+    R.rank = rank; R.n = n; R.nb = nb; R.r = r; R.c = c; R.world = r * c; R.threads = threads;
     R.mc = rank % r; R.mr = rank / r;
     R.lh = len(n, R.mc, r); R.lw = len(n, R.mr, c);
     R.slots = slots; R.slot_elems = slot_elems; R.sh = sh;
