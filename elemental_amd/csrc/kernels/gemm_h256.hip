@@ -695,13 +695,15 @@ __device__ __forceinline__ const uint16_t* tile_base(const uint16_t* X, i64 ld, 
     return KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
 }
 
-template <bool BUF, bool KC>
+// AUX: cache-policy bits of the DMA (0 = default; 17 = sc0 sc1, which hipBLASLt's
+// kernels put on one operand's DirectToLds loads)
+template <bool BUF, bool KC, int AUX = 0>
 __device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int j,
                                       lds_char* img) {
     if constexpr (BUF) {
         const BufferSrc<uint16_t> src(tile_base<KC>(X, ld, R0, k0), (KC ? 256 : BK) * ld * 2);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + j * 1024), 16,
-                                                 off, 0, 0, 0);
+                                                 off, 0, 0, AUX);
     } else {
         glds16(tile_base<KC>(X, ld, R0, k0) + goff, img + j * 1024);
     }
@@ -806,8 +808,8 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
                 if constexpr ((FL & 2048) != 0) {
                     if (u == 0) __builtin_amdgcn_s_setprio(3);
                 }
-                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+                if constexpr (SB) piece<BUF, KCB, (FL & 1024) ? 17 : 0>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BUF, KCA, (FL & 512) ? 17 : 0>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
                 if constexpr ((FL & 2048) != 0) {
                     if (u == 7) __builtin_amdgcn_s_setprio(0);
                 }
@@ -831,7 +833,8 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 // FL: timing ablations only (wrong results): 1 = no staging after the prologue,
 // 2 = no fragment reads, 4 = no barrier, 32 = no wait for the staged K-tile;
 // placement variants (correct): 128, 256 (kstep); 2048 = s_setprio 3 over the
-// staging pieces of each k-step (hipBLASLt's loop raises the priority there)
+// staging pieces of each k-step (hipBLASLt's loop raises the priority there; no
+// gain); 512 / 1024 = A / B staged with the sc0 sc1 cache policy
 template <bool BF16, bool KCA, bool KCB, bool BUF, int FL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
@@ -1008,7 +1011,8 @@ hipError_t launch_h256(const H2Params& p, hipStream_t s) {
             if (buf && fl == 128) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 128>);
             if (buf && fl == 256) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 256>);
             if (buf && fl == 2048) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2048>);
-            if (buf && fl == 2304) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 2304>);
+            if (buf && fl == 512) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 512>);
+            if (buf && fl == 1024) return go(gemm_h4w_kernel<BF16, KCA, KCB, true, 1024>);
         }
         return buf ? go(gemm_h4w_kernel<BF16, KCA, KCB, true>) : go(gemm_h4w_kernel<BF16, KCA, KCB, false>);
     }
