@@ -11,11 +11,21 @@ from elemental_amd import el
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free rendezvous port below the kernel's ephemeral range (32768-60999):
+    a port picked by bind(0) comes from that range, and the outgoing gloo sockets
+    of the test before can take it again before the store listens (EADDRINUSE)."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-32000")
 
 
 def _spawn(fn, world, *args):

@@ -20,11 +20,19 @@ WATCHDOG_EXIT = 75
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port below the ephemeral range (see tests/test_dist_cpu.py)."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-32000")
 
 
 def _run(*args, timeout=60):

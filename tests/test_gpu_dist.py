@@ -17,11 +17,21 @@ pytestmark = pytest.mark.gpu
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free rendezvous port below the kernel's ephemeral range (32768-60999):
+    a port picked by bind(0) comes from that range, and the outgoing gloo sockets
+    of the test before can take it again before the store listens (EADDRINUSE)."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-32000")
 
 
 def _spawn(fn, world, *args):
@@ -315,11 +325,7 @@ def test_gpu_rccl_watchdog_aborts_overrunning_stage():
 def test_gpu_initialize_rccl_world_from_launcher_env():
     """El::Initialize under torch.distributed.run's variables builds COMM_WORLD
     over RCCL (unique id through the TCP rendezvous; size 1 on this box)."""
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = _port()
     p = _failsafe("init_env", env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
                                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     assert p.returncode == 0, p.stdout + p.stderr
