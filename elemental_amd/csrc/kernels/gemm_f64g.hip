@@ -309,7 +309,11 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // wave tile: 64 x 64 (four waves) measured +1.5-2 % for NN/TN/TT; NT (both
     // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();
-    const int wtm = wtm_env ? wtm_env : (!ta && tb) ? 32 : 64;
+    // and with at most one workgroup per CU (a grid of <= 256 tiles x chunks) the
+    // eight-wave 32 x 64 split keeps two waves per SIMD: 2048^3 NN 61.0 -> 64.0 TF
+    // (4096^3 and up: the four-wave split stays ahead; profiles/r03_f64_small.log)
+    const i64 grid_wgs = (i64)((m + 127) / 128) * p.tiles_n * ((kmain + kchunk - 1) / kchunk);
+    const int wtm = wtm_env ? wtm_env : ((!ta && tb) || grid_wgs <= 256) ? 32 : 64;
     // ELX_F64G_DEEP=1: grids of at most one workgroup per CU (no split-k) take the
     // 32-deep slabs on the first kmain/32*32 of k, an odd 16 through the 16-deep
     // kernel (beta = 1).  Off by default: 2048^3 NN 53.8 vs 60.6 TF with the
