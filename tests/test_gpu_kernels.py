@@ -181,6 +181,42 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape):
     assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
+@pytest.mark.parametrize("dt", ["f64", "f32", "bf16", "f16"])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T")])
+def test_local_gemm_matches_vendor_blas(dt, ta, tb):
+    """The same column-major product through the vendor GPU BLAS (torch.matmul ->
+    hipBLASLt, the library family of the reference's rocblas_{d,s,h}gemm calls,
+    src/hydrogen/device/rocBLAS_API.cpp:151-170): both within the north_star
+    bound of the exact product and of each other.  For bf16 this is the only
+    anchor besides the exact-integer test (the reference's CPU path has no bf16)."""
+    m, n, k = 2304, 2056, 1088  # the large-tile kernels, ragged in n
+    tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[dt]
+    eps = {"f64": 2.0 ** -53, "f32": 2.0 ** -24, "bf16": 2.0 ** -8, "f16": 2.0 ** -11}[dt]
+    g = torch.Generator(device="cuda").manual_seed(7)
+    Ash = (m, k) if ta == "N" else (k, m)
+    Bsh = (k, n) if tb == "N" else (n, k)
+    # column-major storage = the transpose of a row-major torch tensor
+    At = (torch.rand(Ash[1], Ash[0], device="cuda", generator=g, dtype=torch.float64) - 0.5).to(tdt)
+    Bt = (torch.rand(Bsh[1], Bsh[0], device="cuda", generator=g, dtype=torch.float64) - 0.5).to(tdt)
+    C = torch.zeros(n, m, device="cuda", dtype=tdt)  # C^T row-major = C column-major
+    fn = {"f64": L.lib().elx_gemm_f64, "f32": L.lib().elx_gemm_f32, "bf16": L.lib().elx_gemm_bf16,
+          "f16": L.lib().elx_gemm_f16}[dt]
+    torch.cuda.synchronize()
+    L.check(fn(OPS[ta], OPS[tb], m, n, k, 1.0, At.data_ptr(), Ash[0], Bt.data_ptr(), Bsh[0], 0.0, C.data_ptr(), m,
+               None))
+    sync()
+    opA = At.t() if ta == "N" else At   # op(A), m x k
+    opB = Bt.t() if tb == "N" else Bt   # op(B), k x n
+    vend = torch.matmul(opA, opB)
+    exact = opA.double() @ opB.double()
+    ours = C.t().double()
+    Ah, Bh = opA.double().cpu().numpy(), opB.double().cpu().numpy()
+    r_ours = oracle.parity_ratio(ours.cpu().numpy(), exact.cpu().numpy(), Ah, Bh, k, eps)
+    r_vend = oracle.parity_ratio(vend.double().cpu().numpy(), exact.cpu().numpy(), Ah, Bh, k, eps)
+    r_pair = oracle.parity_ratio(ours.cpu().numpy(), vend.double().cpu().numpy(), Ah, Bh, k, eps)
+    assert r_ours <= 10 and r_pair <= 10, f"{dt} {ta}{tb}: ours {r_ours:.3g} vendor {r_vend:.3g} pair {r_pair:.3g}"
+
+
 def test_local_gemm_16bit_group_knob_clamped(monkeypatch):
     """ELX_H16_GROUP (the tile-order group height, read per call) of 0 or garbage
     must not reach the kernel's tile mapping, which divides by it: a zero height
