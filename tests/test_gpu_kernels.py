@@ -149,13 +149,14 @@ def test_local_gemm_16bit(kind, ta, tb, shape):
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-@pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640)])
+@pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64)])
 def test_local_gemm_16bit_exact(kind, ta, tb, shape):
     """Integer operands in [-2, 2]: every partial sum is exact in the f32
     accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
     to 16 bits, and the result must equal numpy's rounding of the exact value bit
     for bit.  k = 2112: 66 slabs of 32 (the 16-bit kernels' main loop over many
-    wraps of their LDS ring); 2312 columns: ragged edge tiles.  (k a multiple of
+    wraps of their LDS ring); 2312 columns: ragged edge tiles; k = 64: a single
+    K-tile (the ring's prologue and clamped restaging only).  (k a multiple of
     64: a k tail is a second pass that adds to the already rounded C.)"""
     m, n, k = shape
     rng = np.random.default_rng(m + n + k)
