@@ -209,9 +209,14 @@ hipError_t launch_fw(const FParams& p, hipStream_t s) {
 
 template <bool KCA, bool KCB, bool BUF>
 hipError_t launch_fb(const FParams& p, hipStream_t s) {
-    // 64 x 64 wave tiles (the fp64 kernel's choice) measured a wash here: within
-    // -2 .. +1.7 % of 32 x 64 across shapes (profiles/r01_f32_wave.log)
-    static const int wtm = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 32; }();
+    // 64 x 64 wave tiles (the fp64 kernel's choice) measured a wash on square
+    // shapes: within -2 .. +1.7 % of 32 x 64 (profiles/r01_f32_wave.log).  Both
+    // operands k-contiguous with a long k per tile (C4's TN, k = 524288 whole or
+    // in split-k chunks of 131072) is the exception: 64 x 64 gains 2.5-5.5 %
+    // from k = 65536 up (141 -> 149 TF at 8192^2 x 524288; k = 16384 -0.6 %;
+    // profiles/r03_f32_wtm.log)
+    static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
+    const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
     if (wtm == 64) return launch_fw<64, KCA, KCB, BUF>(p, s);
     return launch_fw<32, KCA, KCB, BUF>(p, s);
 }

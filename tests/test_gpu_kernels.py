@@ -218,6 +218,27 @@ def test_local_gemm_matches_vendor_blas(dt, ta, tb):
     assert r_ours <= 10 and r_pair <= 10, f"{dt} {ta}{tb}: ours {r_ours:.3g} vendor {r_vend:.3g} pair {r_pair:.3g}"
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k,beta", [(2994, 2900, 32837, 0.0), (1000, 1030, 524325, -2.0)])
+def test_local_gemm_f32_tn_long_k_exact(m, n, k, beta):
+    """f32 TN with a long k per tile takes the 64 x 64 wave tiles (C4's shape,
+    gemm_f32g.hip launch_fb): the first case as one launch over 552 tiles, the
+    second split-k into 16 chunks of 32768 plus the k tail, with beta != 0.
+    Integer operands in [-2, 2] keep every partial sum below 2^24, so the f32
+    result is exact and must equal the f64 product bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    At = torch.randint(-2, 3, (m, k), device="cuda", generator=g).float()  # column-major k x m = op(A)^T
+    Bt = torch.randint(-2, 3, (n, k), device="cuda", generator=g).float()  # column-major k x n
+    C0 = torch.randint(-3, 4, (n, m), device="cuda", generator=g).float()  # C^T row-major = C column-major
+    C = C0.clone()
+    torch.cuda.synchronize()
+    L.check(L.lib().elx_gemm_f32(OPS["T"], OPS["N"], m, n, k, 1.0, At.data_ptr(), k, Bt.data_ptr(), k, beta, C.data_ptr(), m,
+                                 None))
+    sync()
+    want = (Bt.double() @ At.double().t() + beta * C0.double()).float()  # (A^T B)^T = B^T A, n x m
+    assert torch.equal(C, want), f"max err {(C - want).abs().max().item()}"
+
+
 def test_local_gemm_16bit_group_knob_clamped(monkeypatch):
     """ELX_H16_GROUP (the tile-order group height, read per call) of 0 or garbage
     must not reach the kernel's tile mapping, which divides by it: a zero height
