@@ -36,7 +36,8 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
     // slabs); with fewer tiles than CUs, chunks down to 256 (1024^3 f64: 64 tiles
     // -> 4 chunks, 150 -> 60 us; at 2048^3, 256 tiles, chunks of 512 measured
     // slower than none: the partials' HBM round trip outweighs the fill)
-    const i64 min_chunk = tiles < 256 ? 256 : 2048;
+    static const i64 min_env = [] { const char* v = getenv("ELX_DMA_MIN_CHUNK"); return v ? atoll(v) : 0ll; }();
+    const i64 min_chunk = min_env >= bk ? min_env : tiles < 256 ? 256 : 2048;
     i64 z = (2 * slots + tiles - 1) / tiles;
     z = z < d.kmain / min_chunk ? z : d.kmain / min_chunk;
     z = z < 16 ? z : 16;
