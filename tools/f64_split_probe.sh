@@ -1,13 +1,12 @@
 #!/bin/bash
-# f64 one-workgroup-per-CU grids (2048^3: 256 tiles): split-k in 2 chunks
-# (ELX_DMA_MIN_CHUNK=1024) vs none (default) vs 4 chunks (512)
+# split-k chunk count for grids below two workgroups per CU: with k = 2048 the
+# min-chunk knob sets z = min(ceil(1024 / tiles), 2048 / chunk): 1024 -> 2,
+# 683 -> 3, 512 -> 4, 342 -> 6 (capped by the first term), 256 -> 8; 0 = rule
 set -e
 cd "$(dirname "$0")/.."
-S="f64,0,0,2048,2048,2048 f64,1,0,2048,2048,2048 f64,0,0,2048,2048,4096 f64,0,0,1536,2048,2048 f32,0,0,2048,2048,2048"
-for r in 1 2; do
-for c in 0 1024 512; do
+S="f64,0,0,1024,1024,2048 f64,0,0,1536,1536,2048 f64,0,0,1536,2048,2048 f64,0,0,1920,2048,2048 f64,0,0,1536,2048,4096 f32,0,0,1536,2048,2048 f32,0,0,1024,1024,2048"
+for c in 0 1024 683 512 342 256; do
 echo "== min chunk $c"
 ELX_DMA_MIN_CHUNK=$c timeout -k 10 200 python -u tools/gemm_bench.py $S
-done
 done
 timeout -k 10 200 python -u tools/gemm_bench.py $S --vendor
