@@ -39,6 +39,11 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
     static const i64 min_env = [] { const char* v = getenv("ELX_DMA_MIN_CHUNK"); return v ? atoll(v) : 0ll; }();
     const i64 min_chunk = min_env >= bk ? min_env : tiles < 256 ? 256 : 2048;
     i64 z = (2 * slots + tiles - 1) / tiles;
+    // 33..255 tiles (one workgroup per CU or fewer): 4 chunks up to 200 tiles, 2
+    // above, measured best of 2..8 (f64 1024^2 x 2048 44.7 -> 49.4 TF, 1536 x 2048 x
+    // 2048 47.4 -> 54.7, 1920 x 2048 x 2048 51.0 -> 57.4; f32 likewise;
+    // profiles/r03_f64_small.log).  Fewer tiles keep two rounds of workgroups.
+    if (tiles > 32 && tiles < 256) z = tiles <= 200 ? 4 : 2;
     z = z < d.kmain / min_chunk ? z : d.kmain / min_chunk;
     z = z < 16 ? z : 16;
     if (z < 2) {

@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 S="f64,0,0,1024,1024,2048 f64,0,0,1536,1536,2048 f64,0,0,1536,2048,2048 f64,0,0,1920,2048,2048 f64,0,0,1536,2048,4096 f32,0,0,1536,2048,2048 f32,0,0,1024,1024,2048"
-for c in 0 1024 683 512 342 256; do
+for c in ${CHUNKS:-0 1024 683 512 342 256}; do
 echo "== min chunk $c"
 ELX_DMA_MIN_CHUNK=$c timeout -k 10 200 python -u tools/gemm_bench.py $S
 done
