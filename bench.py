@@ -202,19 +202,21 @@ def est_seconds(flops: float, dtype: str, world: int) -> float:
 
 
 def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n: int = 65536,
-               kc: int = 8192) -> dict:
-    """C3 (El::Gemm NN fp64 m=n=k=65536) on a 1x1 grid through the panel path:
+               kc: int = 8192, dtype: str = "f64") -> dict:
+    """C3 (El::Gemm NN fp64 / fp32 m=n=k=65536) on a 1x1 grid through the panel path:
     k in uniform kc-deep compute panels (8 launches of 65536^2 x 8192).  The
     1x2 / 2x2 / 2x4 grids gather their panels and ramp the first ones (kc/4,
     kc/2, kc, ..., gemm.cpp SummaC), so they run 9 launches whose first two are
     shallower; value_N / (N * value) is a same-problem strong-scaling
     efficiency that charges that ramp to the N > 1 side."""
     el.SetComputePanel(kc)
-    stage("c3_1gpu", 120 + 4 * (steps + warmup) * est_seconds(2.0 * n ** 3, "f64", 1))
+    DT = {"f64": el.F64, "f32": el.F32}[dtype]
+    name = "c3_1gpu" if dtype == "f64" else f"c3_1gpu_{dtype}"
+    stage(name, 120 + 4 * (steps + warmup) * est_seconds(2.0 * n ** 3, dtype, 1))
     try:
-        A = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(1, 0.0, 0.1)
-        B = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(2, 0.0, 0.1)
-        C = el.DistMatrix(grid, el.F64, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(3, 0.0, 0.1)
+        A = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(1, 0.0, 0.1)
+        B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(2, 0.0, 0.1)
+        C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=n, width=n).fill_hash(3, 0.0, 0.1)
         for _ in range(warmup):
             el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C)
         barrier()
@@ -227,28 +229,30 @@ def c3_one_gpu(el, L, grid, barrier, steps: int, warmup: int, kc_restore: int, n
         elapsed = time.perf_counter() - t0
         prof = profile_summary(L, ctypes)
         L.call("elx_set_profiling", 0)
-        stage("c3_1gpu verify", 120 + 4 * est_seconds(2.0 * n ** 3, "f64", 1))
-        check = verify_point(el, grid, el.F64, "f64", el.NORMAL,
+        stage(f"{name} verify", 120 + 4 * est_seconds(2.0 * n ** 3, dtype, 1))
+        check = verify_point(el, grid, DT, dtype, el.NORMAL,
                              lambda: el.Gemm(el.NORMAL, el.NORMAL, 0.5, A, B, -0.5, C), A, B, C, n)
+        del A, B, C
     finally:
         el.SetComputePanel(kc_restore)
     value = 2.0 * n ** 3 * steps / elapsed / 1e12
     avg_ms = prof["gemm_ms"] / max(prof["launches"], 1)
     fpl = prof["flops"] / max(prof["launches"], 1)
     ach = fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    return {"workload": f"C3 on 1 GPU: El::Gemm NN f64 m=n=k={n}, Grid 1x1, compute panel kc={kc} "
+    return {"workload": f"C3 on 1 GPU: El::Gemm NN {dtype} m=n=k={n}, Grid 1x1, compute panel kc={kc} "
                         f"({n // kc} uniform MFMA launches per step; grids > 1x1 ramp the first panels kc/4, kc/2)",
-            "value": round(value, 3), "unit": "TFLOP/s", "steps": steps, "warmup": warmup,
+            "value": round(value, 3), "unit": "TFLOP/s", "dtype": dtype, "steps": steps, "warmup": warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3),
-            "pct_of_mfma_peak": round(100.0 * value / PEAK_TFLOPS["f64"], 2),
-            "roofline": {"bound": "mfma", "kernel": KERNEL["f64"], "achieved": round(ach, 3),
-                         "peak": PEAK_TFLOPS["f64"], "frac": round(ach / PEAK_TFLOPS["f64"], 4),
+            "pct_of_mfma_peak": round(100.0 * value / PEAK_TFLOPS[dtype], 2),
+            "roofline": {"bound": "mfma", "kernel": KERNEL[dtype], "achieved": round(ach, 3),
+                         "peak": PEAK_TFLOPS[dtype], "frac": round(ach / PEAK_TFLOPS[dtype], 4),
                          "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)},
             "exposed_compute_gap_ms_per_step": round(prof["gap_ms"] / max(steps, 1), 3),
             "verify": check}
 
 
-def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: int, world: int, size: int = 0) -> dict:
+def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: int, world: int, size: int = 0,
+                 half: str = "bf16") -> dict:
     """The other BASELINE configs as sub-results of the default line (evidence
     beside the driver's C2 / C3 value, measured in the same run on the same
     grid): C4, TN fp32 m=n=8192 k=524288*N with [VC,STAR] inputs (SUMMA_DOT,
@@ -265,12 +269,13 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
         workload = f"C4: El::Gemm TN f32 m=n={m} k={k} (SUMMA_DOT), A,B [VC,STAR], Grid {gshape}"
     else:
         m = n = k = size or 32768
-        DT, dtype, oA = el.BF16, "bf16", el.NORMAL
+        DT, dtype, oA = {"bf16": el.BF16, "f16": el.F16}[half], half, el.NORMAL
         A = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=k).fill_hash(1, 0.0, 0.1)
         B = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=k, width=n).fill_hash(2, 0.0, 0.1)
-        workload = f"C5: El::Gemm NN bf16 m=n=k={m} on [MC,MR], Grid {gshape}"
+        workload = f"C5: El::Gemm NN {half} m=n=k={m} on [MC,MR], Grid {gshape}"
     C = el.DistMatrix(grid, DT, el.MC, el.MR, el.GPU, height=m, width=n).fill_hash(3, 0.0, 0.1)
-    stage(config, 120 + 4 * (warmup + steps) * est_seconds(2.0 * m * n * k, dtype, world))
+    sname = config if dtype in ("f32", "bf16") else f"{config}_{dtype}"
+    stage(sname, 120 + 4 * (warmup + steps) * est_seconds(2.0 * m * n * k, dtype, world))
     for _ in range(warmup):
         el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C)
     barrier()
@@ -294,11 +299,11 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
                         "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)}}
     if world > 1:
         out["collectives"] = collectives_summary(prof, steps)
-    stage(f"{config} verify", 120 + 4 * est_seconds(2.0 * m * n * k, dtype, world))
+    stage(f"{sname} verify", 120 + 4 * est_seconds(2.0 * m * n * k, dtype, world))
     out["verify"] = verify_point(el, grid, DT, dtype, oA, lambda: el.Gemm(oA, el.NORMAL, 0.5, A, B, -0.5, C),
                                  A, B, C, k)
     if config == "c5":
-        stage("c5 entrywise", 120)
+        stage(f"{sname} entrywise", 120)
         loc = A.LocalHeight() * A.LocalWidth()
         ew = {}
         for name, fn in (("axpy", lambda: el.Axpy(0.5, A, C)), ("hadamard", lambda: el.Hadamard(A, B, C))):
@@ -309,7 +314,7 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
                 fn()
             barrier()
             dt = maxr((time.perf_counter() - t1) / 20)
-            gbs = 3 * 2 * loc / dt / 1e9
+            gbs = 3 * 2 * loc / dt / 1e9  # both 16-bit types
             ew[name] = {"ms": round(dt * 1e3, 4), "GB_per_s_per_gpu": round(gbs, 1),
                         "frac_of_hbm": round(gbs / HBM_PEAK_GBS, 4)}
         out["entrywise"] = ew
@@ -506,15 +511,17 @@ def main():
     barrier()
 
     # from here on the line exists: if a later (optional) stage overruns, the
-    # watchdog prints it with that stage marked, and the process exits 0
+    # watchdog prints it with that stage marked and the process still exits
+    # NON-ZERO (ELX_WATCHDOG_EXIT), so a hang is never recorded as success
     def epitaph(pending: str | None):
         if rank != 0:
-            el.watchdog_epitaph("", 0)
+            el.watchdog_epitaph("", el.WATCHDOG_EXIT)
             return
         line = dict(out)
         if pending:
             line[pending] = {"error": f"watchdog: stage {pending} overran its deadline (RCCL aborted)"}
-        el.watchdog_epitaph(json.dumps(line), 0)
+            line["incomplete"] = f"stage {pending} overran; exit status {el.WATCHDOG_EXIT}"
+        el.watchdog_epitaph(json.dumps(line), el.WATCHDOG_EXIT)
 
     def extra(key: str, fn):
         epitaph(key)
@@ -572,14 +579,17 @@ def main():
         # compute panels as EffectivePanel picks on grids > 1x1), on this one GPU
         A = B = C = None  # release the C2 operands before the n = 65536 ones
         extra("c3_1gpu", lambda: c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc))
+        # C3 is "fp64/fp32": the fp32 half of the same problem
+        extra("c3_1gpu_f32", lambda: c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc, dtype="f32"))
     if config in ("c2", "c3") and (not args.n or rehearse) and not args.no_extra_configs:
         # the other BASELINE configs, measured in the same run on the same grid
         # (N = 1: c4_1gpu / c5_1gpu; N > 1: c4 / c5 on Grid::DefaultHeight(N))
         A = B = C = None  # release the main operands (no-op when already released)
-        for cfg, st in (("c4", 2), ("c5", 5)):
-            key = f"{cfg}_1gpu" if world == 1 else cfg
-            extra(key, lambda cfg=cfg, st=st: config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1, world,
-                                                            args.n))
+        # C5 is "bf16/half": both 16-bit types
+        for cfg, st, half in (("c4", 2, "bf16"), ("c5", 5, "bf16"), ("c5", 5, "f16")):
+            key = (f"{cfg}_1gpu" if world == 1 else cfg) + ("_f16" if half == "f16" else "")
+            extra(key, lambda cfg=cfg, st=st, half=half: config_point(el, L, grid, barrier, max_over_ranks, cfg, st, 1,
+                                                                      world, args.n, half))
     if world == 1 and config == "c2" and not args.n and not args.no_extra_configs:
         # C1's problem (NN f64 4096^3) on the GPU, beside the CPU leg's same problem
         def c1():

@@ -60,6 +60,9 @@ _SIGS = {
     "elx_pool_free": (_i, [_vp, _vp]),
     "elx_pool_trim": (_i, [c_size_t]),
     "elx_pool_stats": (_i, [POINTER(c_size_t), POINTER(c_size_t)]),
+    "elx_pool_set_max_cached": (_i, [c_size_t]),
+    "elx_pool_max_cached": (_i, [POINTER(c_size_t)]),
+    "elx_pool_bin_bytes": (c_size_t, [c_size_t]),
     "elx_memcpy_h2d": (_i, [_vp, _vp, c_size_t, _vp]),
     "elx_memcpy_d2h": (_i, [_vp, _vp, c_size_t, _vp]),
     "elx_memcpy_d2d": (_i, [_vp, _vp, c_size_t, _vp]),
@@ -109,6 +112,12 @@ _SIGS = {
     "elx_comm_bcast": (_i, [_vp, _i, _vp, _i64, _i, _vp]),
     "elx_comm_alltoall": (_i, [_vp, _i, _vp, _vp, _i64, _vp]),
     "elx_comm_sendrecv": (_i, [_vp, _i, _vp, _i, _vp, _i, _i64, _vp]),
+    "elx_mpi_allgather": (_i, [_vp, _i, _i, _vp, _vp, c_int64, _vp]),
+    "elx_mpi_reduce_scatter": (_i, [_vp, _i, _i, _i, _vp, _vp, c_int64, _vp]),
+    "elx_mpi_allreduce": (_i, [_vp, _i, _i, _i, _vp, _vp, c_int64, _vp]),
+    "elx_mpi_alltoall": (_i, [_vp, _i, _i, _vp, _vp, c_int64, _vp]),
+    "elx_mpi_bcast": (_i, [_vp, _i, _i, _vp, c_int64, _i, _vp]),
+    "elx_mpi_sendrecv": (_i, [_vp, _i, _i, _vp, c_int64, _i, _vp, c_int64, _i, _vp]),
     "elx_comm_stats": (_i, [POINTER(c_int64), POINTER(c_double), POINTER(c_int64)]),
     "elx_comm_stats_reset": (_i, []),
     "elx_grid_default_height": (_i, [_i]),
@@ -237,4 +246,4 @@ def declared_symbols(header: str | None = None) -> list[str]:
     import re
     header = header or os.path.join(os.path.dirname(_HERE), "include", "elemental_amd.h")
     text = open(header).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int64_t|int)\s+(elx_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int64_t|size_t|int)\s+(elx_\w+)\s*\(", text, re.M)))

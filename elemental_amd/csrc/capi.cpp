@@ -122,6 +122,9 @@ int elx_pool_alloc(void** ptr, size_t bytes, void* stream) {
 int elx_pool_free(void* ptr, void* stream) { return Guard([&] { Runtime::Get().Free(ptr, S(stream)); }); }
 int elx_pool_trim(size_t keep) { return Guard([&] { Runtime::Get().Trim(keep); }); }
 int elx_pool_stats(size_t* reserved, size_t* in_use) { return Guard([&] { Runtime::Get().Stats(*reserved, *in_use); }); }
+int elx_pool_set_max_cached(size_t bytes) { return Guard([&] { Runtime::Get().SetMaxCached(bytes); }); }
+int elx_pool_max_cached(size_t* bytes) { return Guard([&] { *bytes = Runtime::Get().MaxCached(); }); }
+size_t elx_pool_bin_bytes(size_t bytes) { return Runtime::BinBytes(bytes); }
 int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
     return Guard([&] {
         hipStream_t s = S(stream);
@@ -497,6 +500,102 @@ int elx_comm_sendrecv(elx_comm_t c, int dtype, const void* send, int dest, void*
     return Guard([&] {
         ELX_REQUIRE(dest >= 0 && dest < c->c->Size() && src >= 0 && src < c->c->Size(), "sendrecv: peer outside the communicator");
         c->c->SendRecv(ToDType(dtype), send, dest, recv, src, count, CommDev(c), CommStream(c, stream));
+    });
+}
+extern "C++" {
+namespace {
+// El::mpi on explicit-device buffers.  Host buffers over an RCCL communicator of
+// size > 1 go through device copies on the comm stream (RCCL reads device
+// memory only) and the call is synchronous, as the reference's MPI path on
+// Device::CPU is.  `inplace`: send and recv are one buffer (Broadcast).
+template <class F>
+void MpiRun(elx_comm_t c, int device, void* stream, const void* send, size_t sbytes, void* recv, size_t rbytes,
+            bool inplace, F&& f) {
+    ELX_REQUIRE(c && c->c, "null comm");
+    ELX_REQUIRE(device == ELX_DEVICE_CPU || device == ELX_DEVICE_GPU, "unknown device ", device);
+    const Device d = device == ELX_DEVICE_GPU ? Device::GPU : Device::CPU;
+    if (c->c->kind() == Comm::Kind::RCCL && d == Device::CPU && c->c->Size() > 1) {
+        hipStream_t s = Runtime::Get().CommStream();
+        Buffer ds(Device::GPU, inplace ? 0 : std::max<size_t>(sbytes, 1), s);
+        Buffer dr(Device::GPU, std::max<size_t>(rbytes, 1), s);
+        if (inplace) {
+            if (rbytes) ELX_CHECK_HIP(hipMemcpyAsync(dr.data(), recv, rbytes, hipMemcpyHostToDevice, s));
+        } else if (sbytes) {
+            ELX_CHECK_HIP(hipMemcpyAsync(ds.data(), send, sbytes, hipMemcpyHostToDevice, s));
+        }
+        f(inplace ? dr.data() : ds.data(), dr.data(), Device::GPU, s);
+        if (rbytes) ELX_CHECK_HIP(hipMemcpyAsync(recv, dr.data(), rbytes, hipMemcpyDeviceToHost, s));
+        ELX_CHECK_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    f(send, recv, d, d == Device::GPU ? S(stream) : nullptr);
+}
+ReduceOp ToOp(int op) {
+    ELX_REQUIRE(op >= ELX_OP_SUM && op <= ELX_OP_MIN, "unknown reduction op ", op);
+    return static_cast<ReduceOp>(op);
+}
+}  // namespace
+}  // extern "C++"
+int elx_mpi_allgather(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
+                      void* stream) {
+    return Guard([&] {
+        const DType t = ToDType(dtype);
+        const size_t b = static_cast<size_t>(count) * DTypeSize(t);
+        MpiRun(c, device, stream, send, b, recv, b * c->c->Size(), false,
+               [&](const void* sb, void* rb, Device d, hipStream_t s) { c->c->AllGather(t, sb, rb, count, d, s); });
+    });
+}
+int elx_mpi_reduce_scatter(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv,
+                           int64_t count, void* stream) {
+    return Guard([&] {
+        const DType t = ToDType(dtype);
+        const ReduceOp o = ToOp(op);
+        const size_t b = static_cast<size_t>(count) * DTypeSize(t);
+        MpiRun(c, device, stream, send, b * c->c->Size(), recv, b, false,
+               [&](const void* sb, void* rb, Device d, hipStream_t s) { c->c->ReduceScatter(t, sb, rb, count, d, s, o); });
+    });
+}
+int elx_mpi_allreduce(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv, int64_t count,
+                      void* stream) {
+    return Guard([&] {
+        const DType t = ToDType(dtype);
+        const ReduceOp o = ToOp(op);
+        const size_t b = static_cast<size_t>(count) * DTypeSize(t);
+        MpiRun(c, device, stream, send, b, recv, b, false,
+               [&](const void* sb, void* rb, Device d, hipStream_t s) { c->c->AllReduce(t, sb, rb, count, d, s, o); });
+    });
+}
+int elx_mpi_alltoall(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
+                     void* stream) {
+    return Guard([&] {
+        const DType t = ToDType(dtype);
+        const int p = c->c->Size();
+        const size_t b = static_cast<size_t>(count) * DTypeSize(t) * p;
+        std::vector<Int> cnt(p, count), dsp(p);
+        for (int q = 0; q < p; ++q) dsp[q] = (Int)q * count;
+        MpiRun(c, device, stream, send, b, recv, b, false, [&](const void* sb, void* rb, Device d, hipStream_t s) {
+            c->c->AllToAllV(t, sb, cnt, dsp, rb, cnt, dsp, d, s);
+        });
+    });
+}
+int elx_mpi_bcast(elx_comm_t c, int dtype, int device, void* buf, int64_t count, int root, void* stream) {
+    return Guard([&] {
+        ELX_REQUIRE(root >= 0 && root < c->c->Size(), "bcast: root ", root, " outside the communicator");
+        const DType t = ToDType(dtype);
+        const size_t b = static_cast<size_t>(count) * DTypeSize(t);
+        MpiRun(c, device, stream, buf, b, buf, b, true,
+               [&](const void*, void* rb, Device d, hipStream_t s) { c->c->Bcast(t, rb, count, root, d, s); });
+    });
+}
+int elx_mpi_sendrecv(elx_comm_t c, int dtype, int device, const void* send, int64_t scount, int dest, void* recv,
+                     int64_t rcount, int src, void* stream) {
+    return Guard([&] {
+        const DType t = ToDType(dtype);
+        const size_t es = DTypeSize(t);
+        MpiRun(c, device, stream, send, static_cast<size_t>(scount) * es, recv, static_cast<size_t>(rcount) * es,
+               false, [&](const void* sb, void* rb, Device d, hipStream_t s) {
+                   c->c->SendRecv(t, sb, scount, dest, rb, rcount, src, d, s);
+               });
     });
 }
 int elx_comm_stats(int64_t* bytes, double* seconds, int64_t* calls) {

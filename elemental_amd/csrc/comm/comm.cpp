@@ -293,7 +293,19 @@ void Comm::AllGather(DType t, const void* send, void* recv, Int count, Device de
     ELX_CHECK_HIP(hipStreamSynchronize(s));
 }
 
-void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+namespace {
+ncclRedOp_t NcclOp(ReduceOp op) {
+    switch (op) {
+    case ReduceOp::SUM: return ncclSum;
+    case ReduceOp::PROD: return ncclProd;
+    case ReduceOp::MAX: return ncclMax;
+    case ReduceOp::MIN: return ncclMin;
+    }
+    throw LogicError("unknown reduction op");
+}
+}  // namespace
+
+void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s, ReduceOp op) {
     const size_t es = DTypeSize(t), bytes = static_cast<size_t>(count) * es;
     auto& st = GlobalCommStats();
     st.calls++;
@@ -302,10 +314,13 @@ void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Devic
     if (count == 0) return;
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclReduceScatter", nccl_);
+        CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), NcclOp(op), nccl_, s), "ncclReduceScatter", nccl_);
         return;
     }
-    if (t == DType::F16 || t == DType::BF16) { HostSum16(true, t, send, recv, count, dev, s); return; }
+    if (op != ReduceOp::SUM || t == DType::F16 || t == DType::BF16) {
+        HostFold(true, t, op, send, recv, count, dev, s);
+        return;
+    }
     if (dev == Device::CPU) { HostCall(ELX_COLL_REDUCE_SCATTER, t, send, recv, count, 0, 0); return; }
     static Staging stg;
     char* h = static_cast<char*>(stg.Get(bytes * (size_ + 1)));
@@ -316,16 +331,19 @@ void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Devic
     ELX_CHECK_HIP(hipStreamSynchronize(s));
 }
 
-void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s, ReduceOp op) {
     const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
     if (size_ == 1) { CopyBytes(dev, recv, send, bytes, s); return; }
     if (count == 0) return;
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
-        CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), ncclSum, nccl_, s), "ncclAllReduce", nccl_);
+        CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), NcclOp(op), nccl_, s), "ncclAllReduce", nccl_);
         return;
     }
-    if (t == DType::F16 || t == DType::BF16) { HostSum16(false, t, send, recv, count, dev, s); return; }
+    if (op != ReduceOp::SUM || t == DType::F16 || t == DType::BF16) {
+        HostFold(false, t, op, send, recv, count, dev, s);
+        return;
+    }
     if (dev == Device::CPU) { HostCall(ELX_COLL_ALLREDUCE, t, send, recv, count, 0, 0); return; }
     static Staging stg;
     char* h = static_cast<char*>(stg.Get(bytes * 2));
@@ -337,13 +355,36 @@ void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device de
 }
 
 // Every rank gathers the contributions it reduces (ALLTOALL of its slice for
-// a reduce-scatter, ALLGATHER for an all-reduce) and folds them in rank order,
-// each addition done in float and rounded back to 16 bits, as
-// GPUHalfSumFunc's out[i] = float(in[i]) + float(out[i]) (environment.cpp:135-142).
-void Comm::HostSum16(bool scatter, DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s) {
+// a reduce-scatter, ALLGATHER for an all-reduce) and folds them in rank order.
+// 16-bit: each step in float, rounded back to 16 bits, as GPUHalfSumFunc's
+// out[i] = float(in[i]) + float(out[i]) (environment.cpp:135-142).
+namespace {
+template <typename V>
+V FoldOp(ReduceOp op, V acc, V x) {
+    switch (op) {
+    case ReduceOp::SUM: return x + acc;
+    case ReduceOp::PROD: return x * acc;
+    case ReduceOp::MAX: return acc < x ? x : acc;
+    case ReduceOp::MIN: return x < acc ? x : acc;
+    }
+    return acc;
+}
+template <typename E>
+void FoldRanks(ReduceOp op, const char* gathered, char* out, Int count, int size) {
+    const E* g = reinterpret_cast<const E*>(gathered);
+    E* o = reinterpret_cast<E*>(out);
+    for (Int i = 0; i < count; ++i) o[i] = g[i];
+    for (int r = 1; r < size; ++r)
+        for (Int i = 0; i < count; ++i) o[i] = FoldOp(op, o[i], g[r * count + i]);
+}
+}  // namespace
+
+void Comm::HostFold(bool scatter, DType t, ReduceOp op, const void* send, void* recv, Int count, Device dev,
+                    hipStream_t s) {
     const size_t es = DTypeSize(t);
     const Int sendCount = scatter ? count * size_ : count;
-    std::vector<uint16_t> hs(static_cast<size_t>(sendCount)), hr(static_cast<size_t>(count) * size_);
+    std::vector<char> hs(static_cast<size_t>(sendCount) * es), hr(static_cast<size_t>(count) * size_ * es),
+        out(static_cast<size_t>(count) * es);
     if (dev == Device::GPU) {
         ELX_CHECK_HIP(hipMemcpyAsync(hs.data(), send, sendCount * es, hipMemcpyDeviceToHost, s));
         ELX_CHECK_HIP(hipStreamSynchronize(s));
@@ -351,12 +392,20 @@ void Comm::HostSum16(bool scatter, DType t, const void* send, void* recv, Int co
         std::memcpy(hs.data(), send, sendCount * es);
     }
     HostCall(scatter ? ELX_COLL_ALLTOALL : ELX_COLL_ALLGATHER, t, hs.data(), hr.data(), count, 0, 0);
-    const bool bf = t == DType::BF16;
-    auto ld = [&](uint16_t v) { return bf ? BF16ToFloat(v) : HalfToFloat(v); };
-    auto st = [&](float v) { return bf ? FloatToBF16(v) : FloatToHalf(v); };
-    std::vector<uint16_t> out(hr.begin(), hr.begin() + count);
-    for (int r = 1; r < size_; ++r)
-        for (Int i = 0; i < count; ++i) out[i] = st(ld(hr[r * count + i]) + ld(out[i]));
+    if (t == DType::F64) {
+        FoldRanks<double>(op, hr.data(), out.data(), count, size_);
+    } else if (t == DType::F32) {
+        FoldRanks<float>(op, hr.data(), out.data(), count, size_);
+    } else {
+        const bool bf = t == DType::BF16;
+        auto ld = [&](uint16_t v) { return bf ? BF16ToFloat(v) : HalfToFloat(v); };
+        auto stv = [&](float v) { return bf ? FloatToBF16(v) : FloatToHalf(v); };
+        const uint16_t* g = reinterpret_cast<const uint16_t*>(hr.data());
+        uint16_t* o = reinterpret_cast<uint16_t*>(out.data());
+        for (Int i = 0; i < count; ++i) o[i] = g[i];
+        for (int r = 1; r < size_; ++r)
+            for (Int i = 0; i < count; ++i) o[i] = stv(FoldOp(op, ld(o[i]), ld(g[r * count + i])));
+    }
     if (dev == Device::GPU) {
         ELX_CHECK_HIP(hipMemcpyAsync(recv, out.data(), count * es, hipMemcpyHostToDevice, s));
         ELX_CHECK_HIP(hipStreamSynchronize(s));
@@ -546,23 +595,38 @@ void Comm::HostGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s) {
 }
 
 void Comm::SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s) {
-    const size_t bytes = static_cast<size_t>(count) * DTypeSize(t);
+    SendRecv(t, send, count, dest, recv, count, src, dev, s);
+}
+
+void Comm::SendRecv(DType t, const void* send, Int scount, int dest, void* recv, Int rcount, int src, Device dev,
+                    hipStream_t s) {
+    const size_t es = DTypeSize(t);
     ELX_REQUIRE(dest >= 0 && dest < size_ && src >= 0 && src < size_, "SendRecv: bad peer ", dest, "/", src, " of ",
                 size_);
+    ELX_REQUIRE(scount >= 0 && rcount >= 0, "SendRecv: negative count");
     auto& st = GlobalCommStats();
     st.calls++;
-    if (src != rank_) st.bytes += static_cast<int64_t>(bytes);
-    if (count == 0) return;
-    if (dest == rank_ && src == rank_) { CopyBytes(dev, recv, send, bytes, s); return; }
+    if (src != rank_) st.bytes += static_cast<int64_t>(rcount * es);
+    if (dest == rank_ && src == rank_) {
+        ELX_REQUIRE(scount == rcount, "SendRecv to self: send count ", scount, " != receive count ", rcount);
+        CopyBytes(dev, recv, send, static_cast<size_t>(rcount) * es, s);
+        return;
+    }
     if (kind_ == Kind::RCCL) {
         ELX_REQUIRE(dev == Device::GPU, "RCCL collectives need device buffers");
+        if (scount == 0 && rcount == 0) return;
         const ncclDataType_t nt = NcclType(t);
         CheckNccl(ncclGroupStart(), "ncclGroupStart");
-        CheckNccl(ncclSend(send, count, nt, dest, nccl_, s), "ncclSend", nccl_);
-        CheckNccl(ncclRecv(recv, count, nt, src, nccl_, s), "ncclRecv", nccl_);
+        if (scount > 0) CheckNccl(ncclSend(send, scount, nt, dest, nccl_, s), "ncclSend", nccl_);
+        if (rcount > 0) CheckNccl(ncclRecv(recv, rcount, nt, src, nccl_, s), "ncclRecv", nccl_);
         CheckNccl(ncclGroupEnd(), "ncclGroupEnd", nccl_);
         return;
     }
+    ELX_REQUIRE(scount == rcount, "SendRecv on the host backend needs equal send and receive counts (",
+                scount, " vs ", rcount, ")");
+    const Int count = scount;
+    const size_t bytes = static_cast<size_t>(count) * es;
+    if (count == 0) return;
     if (dev == Device::CPU) { HostCall(ELX_COLL_SENDRECV, t, send, recv, count, dest, src); return; }
     static Staging stg;
     char* h = static_cast<char*>(stg.Get(bytes * 2));
@@ -647,48 +711,86 @@ struct Fd {
 };
 }  // namespace
 
+// Handshake: each client sends kRdvMagic, its rank and the world size; rank 0
+// serves each valid rank in 1..size-1 once and drops anything else (a stray
+// connection never uses up a peer's slot, and the id is sent only to peers
+// that name this rendezvous).  Rank 0 binds the address the peers dial
+// (MASTER_ADDR; INADDR_ANY only if that address is not local).
+namespace {
+constexpr char kRdvMagic[8] = {'E', 'L', 'X', 'R', 'D', 'V', '0', '1'};
+struct RdvHello {
+    char magic[8];
+    int32_t rank, size;
+};
+bool ResolveV4(const char* addr, int port, sockaddr_in& out) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    const std::string ps = std::to_string(port);
+    if (::getaddrinfo(addr && *addr ? addr : "127.0.0.1", ps.c_str(), &hints, &res) != 0 || !res) return false;
+    std::memcpy(&out, res->ai_addr, sizeof(sockaddr_in));
+    ::freeaddrinfo(res);
+    return true;
+}
+}  // namespace
+
 void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s) {
     ELX_REQUIRE(size >= 1 && rank >= 0 && rank < size, "rendezvous: bad rank ", rank, " of ", size);
     ELX_REQUIRE(port > 0 && port < 65536, "rendezvous: bad port ", port);
     if (size == 1) return;
     const double deadline = Now() + timeout_s;
+    sockaddr_in sa{};
+    if (!ResolveV4(addr, port, sa)) throw CommError(Cat("rendezvous: cannot resolve ", addr ? addr : "(null)"));
     if (rank == 0) {
         Fd ls;
         ls.fd = ::socket(AF_INET, SOCK_STREAM, 0);
         if (ls.fd < 0) throw CommError("rendezvous: socket() failed");
         const int one = 1;
         ::setsockopt(ls.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-        sockaddr_in sa{};
-        sa.sin_family = AF_INET;
-        sa.sin_addr.s_addr = htonl(INADDR_ANY);
-        sa.sin_port = htons(static_cast<uint16_t>(port));
-        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0)
-            throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
+        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0) {
+            if (errno != EADDRNOTAVAIL)
+                throw CommError(Cat("rendezvous: bind to ", addr, ":", port, " failed: ", std::strerror(errno)));
+            sockaddr_in any = sa;  // MASTER_ADDR names another interface (NAT, alias): listen on all
+            any.sin_addr.s_addr = htonl(INADDR_ANY);
+            if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&any), sizeof(any)) != 0)
+                throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
+        }
         if (::listen(ls.fd, size) != 0) throw CommError("rendezvous: listen() failed");
-        for (int served = 1; served < size; ++served) {
+        std::vector<bool> served(size, false);
+        int left = size - 1;
+        while (left > 0) {
             pollfd pf{ls.fd, POLLIN, 0};
-            const int left = static_cast<int>(std::max(0.0, deadline - Now()) * 1000);
-            if (::poll(&pf, 1, left) <= 0)
-                throw CommError(Cat("rendezvous: only ", served - 1, " of ", size - 1, " peers connected in time"));
+            const int ms = static_cast<int>(std::max(0.0, deadline - Now()) * 1000);
+            if (::poll(&pf, 1, ms) <= 0)
+                throw CommError(Cat("rendezvous: only ", size - 1 - left, " of ", size - 1, " peers connected in time"));
             Fd peer;
             peer.fd = ::accept(ls.fd, nullptr, nullptr);
-            if (peer.fd < 0) throw CommError("rendezvous: accept() failed");
+            if (peer.fd < 0) continue;
+            RdvHello h{};
+            try {
+                RecvAll(peer.fd, reinterpret_cast<char*>(&h), sizeof(h), std::min(deadline, Now() + 5.0));
+            } catch (const CommError&) {
+                continue;  // silent or short: not a peer
+            }
+            if (std::memcmp(h.magic, kRdvMagic, sizeof(kRdvMagic)) != 0 || h.size != size || h.rank < 1 ||
+                h.rank >= size || served[h.rank])
+                continue;
             SendAll(peer.fd, static_cast<const char*>(data), bytes);
+            served[h.rank] = true;
+            --left;
         }
         return;
     }
-    addrinfo hints{}, *res = nullptr;
-    hints.ai_family = AF_INET;
-    hints.ai_socktype = SOCK_STREAM;
-    const std::string ps = std::to_string(port);
-    if (::getaddrinfo(addr && *addr ? addr : "127.0.0.1", ps.c_str(), &hints, &res) != 0 || !res)
-        throw CommError(Cat("rendezvous: cannot resolve ", addr));
-    std::unique_ptr<addrinfo, void (*)(addrinfo*)> guard(res, ::freeaddrinfo);
+    RdvHello hello{};
+    std::memcpy(hello.magic, kRdvMagic, sizeof(kRdvMagic));
+    hello.rank = rank;
+    hello.size = size;
     for (;;) {  // rank 0 may not be listening yet
         Fd s;
         s.fd = ::socket(AF_INET, SOCK_STREAM, 0);
         if (s.fd < 0) throw CommError("rendezvous: socket() failed");
-        if (::connect(s.fd, res->ai_addr, res->ai_addrlen) == 0) {
+        if (::connect(s.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0) {
+            SendAll(s.fd, reinterpret_cast<const char*>(&hello), sizeof(hello));
             RecvAll(s.fd, static_cast<char*>(data), bytes, deadline);
             return;
         }

@@ -64,6 +64,10 @@ void WatchdogUnregister(ncclComm_t c);
 void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s);
 
 
+// El::mpi::Op for the reductions (include/El/core/imports/mpi.hpp:88-99): the
+// ops an RCCL reduction supports natively
+enum class ReduceOp : int { SUM = ELX_OP_SUM, PROD = ELX_OP_PROD, MAX = ELX_OP_MAX, MIN = ELX_OP_MIN };
+
 class Comm {
 public:
     enum class Kind { SELF, RCCL, HOST };
@@ -84,8 +88,10 @@ public:
 
     // All counts are in elements of `t`; `dev` says where the buffers live.
     void AllGather(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
-    void ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
-    void AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
+    void ReduceScatter(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s,
+                       ReduceOp op = ReduceOp::SUM);
+    void AllReduce(DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s,
+                   ReduceOp op = ReduceOp::SUM);
     void Bcast(DType t, void* buf, Int count, int root, Device dev, hipStream_t s);
     // Irregular all-to-all: sendcounts/recvcounts per peer (elements), with
     // element displacements into send/recv.  Pairs with zero count are skipped.
@@ -110,15 +116,21 @@ public:
     // Point-to-point exchange (El::mpi::SendRecv, src/core/imports/mpi/SendRecv.hpp:9-60):
     // send `count` elements to `dest` while receiving `count` from `src`.
     void SendRecv(DType t, const void* send, int dest, void* recv, int src, Int count, Device dev, hipStream_t s);
+    // separate send / receive counts (SendRecv.hpp:9-35's sc / rc); the host
+    // backend's callback carries one count, so there they must be equal
+    void SendRecv(DType t, const void* send, Int scount, int dest, void* recv, Int rcount, int src, Device dev,
+                  hipStream_t s);
     void Barrier();
 
 private:
     Comm() = default;
     void HostCall(int op, DType t, const void* send, void* recv, Int count, int peer, int peer2);
     void HostGroup(const std::vector<VSet>& sets, Device dev, hipStream_t s);
-    // 16-bit sums on the host backend, independent of what the callback supports
-    // (the reference registers its own MPI_Op, src/core/environment.cpp:135-142,259-298)
-    void HostSum16(bool scatter, DType t, const void* send, void* recv, Int count, Device dev, hipStream_t s);
+    // Host-backend reductions the callback does not do itself (16-bit sums, the
+    // reference's own MPI_Op, src/core/environment.cpp:135-142,259-298; every
+    // non-SUM op): gather the contributions and fold them in rank order
+    void HostFold(bool scatter, DType t, ReduceOp op, const void* send, void* recv, Int count, Device dev,
+                  hipStream_t s);
     Kind kind_ = Kind::SELF;
     int rank_ = 0, size_ = 1;
     ncclComm_t nccl_ = nullptr;

@@ -68,49 +68,156 @@ void Runtime::EnsureGPU() {
     // (ELX_COMM_PRIORITY=0: the compute stream's priority instead; A/B timing)
     const char* pe = getenv("ELX_COMM_PRIORITY");
     ELX_CHECK_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, pe && atoi(pe) == 0 ? lo : hi));
-    ELX_CHECK_HIP(hipDeviceGetDefaultMemPool(&pool_, device_));
-    uint64_t thresh = std::numeric_limits<uint64_t>::max();  // keep freed blocks cached
+    // The library's own backing pool: other default-pool users of the process
+    // (RCCL, the caller's hipMallocAsync) never share its blocks, and the
+    // caching policy above it is ours, not the driver's (runtime.hpp).
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device_;
+    ELX_CHECK_HIP(hipMemPoolCreate(&pool_, &props));
+    uint64_t thresh = 0;  // caching happens in cache_; the backing returns what it is given
     ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolAttrReleaseThreshold, &thresh));
+    int on = 1;
+    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseFollowEventDependencies, &on));
+    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowOpportunistic, &on));
+    if (!max_cached_set_) {
+        // H_CUB_MAX_CACHED_SIZE as the reference reads it (cub.cpp:37-43)
+        for (const char* v : {"ELX_POOL_MAX_CACHED", "H_CUB_MAX_CACHED_SIZE"}) {
+            if (const char* e = std::getenv(v)) { max_cached_ = std::strtoull(e, nullptr, 10); break; }
+        }
+    }
     gpu_ready_ = true;
+}
+
+size_t Runtime::BinBytes(size_t b) {
+    // powers of two up to 1 MiB (CUB bin_growth 2, cub.cpp:21-24), then eight
+    // bins per octave with a 2 MiB floor: ≤ 12.5 % slack on multi-GiB panels
+    if (b <= 512) return 512;
+    if (b <= (size_t(1) << 20)) {
+        size_t p = 512;
+        while (p < b) p <<= 1;
+        return p;
+    }
+    size_t top = size_t(1) << 20;
+    while ((top << 1) <= b) top <<= 1;
+    const size_t step = std::max<size_t>(size_t(2) << 20, top / 8);
+    return (b + step - 1) / step * step;
+}
+
+void* Runtime::Backing(size_t bin, hipStream_t s) {
+    void* p = nullptr;
+    hipError_t e = hipMallocFromPoolAsync(&p, bin, pool_, s);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+        (void)hipGetLastError();
+        ReleaseCachedLocked(0);  // give the cache back and retry once
+        ELX_CHECK_HIP(hipDeviceSynchronize());
+        ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
+        e = hipMallocFromPoolAsync(&p, bin, pool_, s);
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        throw HIPError(Cat("elx_pool_alloc: ", hipGetErrorString(e), " (", bin, " bytes requested, ",
+                           fr, " bytes available, ", tot, " bytes total, ", cached_, " cached)"));
+    }
+    return p;
+}
+
+void Runtime::ReleaseCachedLocked(size_t keep) {
+    // largest blocks first; each goes back to the backing pool on the compute
+    // stream behind its free's event (the freeing stream may be gone by now)
+    while (cached_ > keep && !cache_.empty()) {
+        auto it = std::prev(cache_.end());
+        ELX_CHECK_HIP(hipStreamWaitEvent(compute_, it->second.ready, 0));
+        ELX_CHECK_HIP(hipFreeAsync(it->second.p, compute_));
+        spare_events_.push_back(it->second.ready);
+        cached_ -= it->first;
+        cache_.erase(it);
+    }
 }
 
 void* Runtime::Alloc(size_t bytes, hipStream_t s) {
     EnsureGPU();
     if (bytes == 0) return nullptr;
-    void* p = nullptr;
-    ELX_CHECK_HIP(hipMallocFromPoolAsync(&p, bytes, pool_, s ? s : compute_));
+    if (!s) s = compute_;
+    const size_t bin = BinBytes(bytes);
     std::lock_guard<std::mutex> lk(mu_);
-    live_[p] = bytes;
+    void* p = nullptr;
+    auto [lo, hi] = cache_.equal_range(bin);
+    if (lo != hi) {
+        // prefer a block last used on this stream, then one whose free has
+        // completed, then any (ordered behind its free's event)
+        auto pick = hi;
+        for (auto it = lo; it != hi; ++it)
+            if (it->second.stream == s) { pick = it; break; }
+        if (pick == hi)
+            for (auto it = lo; it != hi; ++it)
+                if (hipEventQuery(it->second.ready) == hipSuccess) { pick = it; break; }
+        if (pick == hi) pick = lo;
+        if (hipEventQuery(pick->second.ready) != hipSuccess)
+            ELX_CHECK_HIP(hipStreamWaitEvent(s, pick->second.ready, 0));
+        p = pick->second.p;
+        spare_events_.push_back(pick->second.ready);
+        cached_ -= bin;
+        cache_.erase(pick);
+    } else {
+        p = Backing(bin, s);
+    }
+    live_[p] = Live{bytes, bin};
     in_use_ += bytes;
+    live_bin_ += bin;
     return p;
 }
 
 void Runtime::Free(void* p, hipStream_t s) {
     if (!p) return;
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        auto it = live_.find(p);
-        if (it == live_.end()) throw LogicError("elx_pool_free: pointer not from this pool");
-        in_use_ -= it->second;
-        live_.erase(it);
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = live_.find(p);
+    if (it == live_.end()) throw LogicError("elx_pool_free: pointer not from this pool");
+    const Live l = it->second;
+    if (!s) s = compute_;
+    if (cached_ + l.bin > max_cached_) {
+        ELX_CHECK_HIP(hipFreeAsync(p, s));  // over the cap: back to the backing pool
+    } else {
+        hipEvent_t ev = nullptr;
+        if (!spare_events_.empty()) { ev = spare_events_.back(); spare_events_.pop_back(); }
+        else ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ELX_CHECK_HIP(hipEventRecord(ev, s));
+        cache_.emplace(l.bin, Cached{p, s, ev});
+        cached_ += l.bin;
     }
-    ELX_CHECK_HIP(hipFreeAsync(p, s ? s : compute_));
+    in_use_ -= l.requested;
+    live_bin_ -= l.bin;
+    live_.erase(it);
 }
 
 void Runtime::Trim(size_t keep) {
     EnsureGPU();
     ELX_CHECK_HIP(hipDeviceSynchronize());
-    ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, keep));
+    std::lock_guard<std::mutex> lk(mu_);
+    ReleaseCachedLocked(keep);
+    ELX_CHECK_HIP(hipDeviceSynchronize());
+    ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
+}
+
+void Runtime::SetMaxCached(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    max_cached_ = bytes;
+    max_cached_set_ = true;
+    if (gpu_ready_) ReleaseCachedLocked(bytes);
+}
+
+size_t Runtime::MaxCached() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return max_cached_;
 }
 
 void Runtime::Stats(size_t& reserved, size_t& in_use) {
-    reserved = 0;
-    if (gpu_ready_) {
-        uint64_t r = 0;
-        if (hipMemPoolGetAttribute(pool_, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess)
-            reserved = r;
-    }
     std::lock_guard<std::mutex> lk(mu_);
+    reserved = live_bin_ + cached_;
     in_use = in_use_;
 }
 

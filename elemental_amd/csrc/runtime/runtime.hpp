@@ -1,11 +1,31 @@
-// Device runtime: device selection, the library's streams, and the
-// hipMallocAsync memory pool that replaces the reference's hipCUB
-// CachingDeviceAllocator (src/core/imports/cub.cpp:1-75; El::Memory mode 1,
+// Device runtime: device selection, the library's streams, and the caching
+// device allocator that replaces the reference's hipCUB CachingDeviceAllocator
+// (src/core/imports/cub.cpp:1-75; El::Memory mode 1,
 // include/El/core/Memory/impl.hpp:113-187).
+//
+// Allocator contract (what `elx_pool_*` promise):
+//  * sizes are rounded to bins (powers of two up to 1 MiB, then eight bins per
+//    octave, at least 2 MiB apart: ≤ 12.5 % slack) and a freed block is cached
+//    under its bin; a request is served from a cached block of exactly its bin;
+//  * reuse is stream-ordered without a host sync: a block freed on stream F and
+//    handed out on stream S makes S wait on the event recorded on F at the free
+//    (CUB's DeviceFree/DeviceAllocate ready-event rule);
+//  * therefore a repeated alloc/free pattern (the SUMMA panel slots, any
+//    steady-state loop) reserves nothing new after its first pass, whichever
+//    streams it allocates and frees on;
+//  * cached bytes are capped by H_CUB_MAX_CACHED_SIZE / ELX_POOL_MAX_CACHED /
+//    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE):
+//    a free that would exceed the cap returns the block to the backing pool;
+//  * the backing store is the library's own hipMemPool (hipMemPoolCreate,
+//    release threshold 0), never the device's default pool shared with other
+//    users of the process; a failed backing allocation releases the cache and
+//    retries once before reporting out-of-memory.
 #pragma once
 #include "../common.hpp"
+#include <map>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 namespace elx {
 
@@ -25,22 +45,34 @@ public:
     // CUs masked off the compute stream for communication kernels (ELX_COMM_CUS)
     int ReservedCUs() { EnsureGPU(); return reserved_cus_; }
 
-    // Stream-ordered pool allocation (hipMallocFromPoolAsync / hipFreeAsync).
+    // Stream-ordered caching allocation (contract above).
     void* Alloc(size_t bytes, hipStream_t s);
     void Free(void* p, hipStream_t s);
     void Trim(size_t keep);
+    // reserved = live + cached bin bytes; in_use = requested bytes still live
     void Stats(size_t& reserved, size_t& in_use);
+    void SetMaxCached(size_t bytes);
+    size_t MaxCached();
+    static size_t BinBytes(size_t bytes);
 
 private:
+    struct Cached { void* p; hipStream_t stream; hipEvent_t ready; };
+    struct Live { size_t requested, bin; };
     Runtime() = default;
+    void* Backing(size_t bin, hipStream_t s);
+    void ReleaseCachedLocked(size_t keep);
     std::mutex mu_;
     bool gpu_ready_ = false;
     int device_ = -1;
     int reserved_cus_ = 0;
     hipStream_t compute_ = nullptr, comm_ = nullptr;
     hipMemPool_t pool_ = nullptr;
-    std::unordered_map<void*, size_t> live_;
-    size_t in_use_ = 0;
+    std::unordered_map<void*, Live> live_;
+    std::multimap<size_t, Cached> cache_;  // bin bytes -> freed block
+    std::vector<hipEvent_t> spare_events_;
+    size_t in_use_ = 0, live_bin_ = 0, cached_ = 0;
+    size_t max_cached_ = ~size_t(0);
+    bool max_cached_set_ = false;
 };
 
 // RAII device or host buffer.  GPU memory comes from the pool on `stream` and is

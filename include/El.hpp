@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <initializer_list>
 #include <memory>
 #include <stdexcept>
@@ -234,9 +235,10 @@ struct SingularMatrixException : std::runtime_error {
 };
 
 namespace detail {
-inline void Check(int rc) {
+// rc's exception; `msg` when the library's last error was overwritten since
+inline void Check(int rc, const std::string& saved = std::string()) {
     if (rc == ELX_OK) return;
-    const std::string msg = elx_last_error();
+    const std::string msg = saved.empty() ? std::string(elx_last_error()) : saved;
     switch (rc) {
     case ELX_ERR_LOGIC: throw LogicError(msg);
     case ELX_ERR_UNSUPPORTED: throw UnsupportedError(msg);
@@ -351,6 +353,111 @@ inline Comm COMM_SELF() { return Comm::Self(); }
 inline int Rank(const Comm& comm = COMM_WORLD) { return comm.Rank(); }
 inline int Size(const Comm& comm = COMM_WORLD) { return comm.Size(); }
 inline void Barrier(const Comm& comm = COMM_WORLD) { detail::Check(elx_comm_barrier(comm.Handle())); }
+
+// ---- typed collectives on SyncInfo-tagged buffers (include/El/core/imports/mpi.hpp) ----
+// Device::GPU: device buffers, enqueued on the SyncInfo's stream after its
+// queued work (RCCL; the host backend stages and synchronizes), as the
+// reference's Aluminum path does; Device::CPU: host buffers, returns when done.
+// El::mpi::Op (mpi.hpp:88-99): the reductions RCCL runs natively.
+struct Op { int code; };
+inline constexpr Op SUM{ELX_OP_SUM};
+inline constexpr Op PROD{ELX_OP_PROD};
+inline constexpr Op MAX{ELX_OP_MAX};
+inline constexpr Op MIN{ELX_OP_MIN};
+namespace detail_ {
+inline void* StreamOf(SyncInfo<Device::CPU> const&) noexcept { return nullptr; }
+inline void* StreamOf(SyncInfo<Device::GPU> const& si) noexcept { return si.Stream(); }
+template <Device D> constexpr int DevCode() noexcept { return static_cast<int>(D); }
+}  // namespace detail_
+
+// Broadcast (mpi.hpp:675-720)
+template <typename T, Device D>
+void Broadcast(T* buffer, int count, int root, Comm const& comm, SyncInfo<D> const& si) {
+    detail::Check(elx_mpi_bcast(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), buffer, count, root,
+                                detail_::StreamOf(si)));
+}
+template <typename T, Device D>
+void Broadcast(T& b, int root, Comm const& comm, SyncInfo<D> const& si) { Broadcast(&b, 1, root, comm, si); }
+
+// AllGather (mpi.hpp:861-930): rbuf holds rc * Size(comm) entries, sc == rc
+template <typename T, Device D>
+void AllGather(T const* sbuf, int sc, T* rbuf, int rc, Comm const& comm, SyncInfo<D> const& si) {
+    if (sc != rc) throw LogicError("AllGather: send and receive counts must match");
+    detail::Check(elx_mpi_allgather(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), sbuf, rbuf, sc,
+                                    detail_::StreamOf(si)));
+}
+
+// AllToAll (mpi.hpp:1006-1075): sc entries to and rc entries from every rank, sc == rc
+template <typename T, Device D>
+void AllToAll(T const* sbuf, int sc, T* rbuf, int rc, Comm const& comm, SyncInfo<D> const& si) {
+    if (sc != rc) throw LogicError("AllToAll: send and receive counts must match");
+    detail::Check(elx_mpi_alltoall(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), sbuf, rbuf, sc,
+                                   detail_::StreamOf(si)));
+}
+
+// AllReduce (mpi.hpp:1248-1351): out-of-place, in-place, default SUM, scalar
+template <typename T, Device D>
+void AllReduce(T const* sbuf, T* rbuf, int count, Op op, Comm const& comm, SyncInfo<D> const& si) {
+    detail::Check(elx_mpi_allreduce(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), op.code, sbuf,
+                                    rbuf, count, detail_::StreamOf(si)));
+}
+template <typename T, Device D>
+void AllReduce(T const* sbuf, T* rbuf, int count, Comm const& comm, SyncInfo<D> const& si) {
+    AllReduce(sbuf, rbuf, count, SUM, comm, si);
+}
+template <typename T, Device D>
+void AllReduce(T* buf, int count, Op op, Comm const& comm, SyncInfo<D> const& si) {
+    AllReduce(static_cast<T const*>(buf), buf, count, op, comm, si);
+}
+template <typename T, Device D>
+void AllReduce(T* buf, int count, Comm const& comm, SyncInfo<D> const& si) { AllReduce(buf, count, SUM, comm, si); }
+// the scalar forms take host values (the reference's one-element overloads)
+template <typename T, Device D>
+T AllReduce(T sb, Op op, Comm const& comm, SyncInfo<D> const&) {
+    T rb = sb;
+    AllReduce(&sb, &rb, 1, op, comm, SyncInfo<Device::CPU>{});
+    return rb;
+}
+template <typename T, Device D>
+T AllReduce(T sb, Comm const& comm, SyncInfo<D> const& si) { return AllReduce(sb, SUM, comm, si); }
+
+// ReduceScatter (mpi.hpp:1361-): sbuf holds rc * Size(comm) entries, rbuf rc
+template <typename T, Device D>
+void ReduceScatter(T const* sbuf, T* rbuf, int rc, Op op, Comm const& comm, SyncInfo<D> const& si) {
+    detail::Check(elx_mpi_reduce_scatter(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), op.code,
+                                         sbuf, rbuf, rc, detail_::StreamOf(si)));
+}
+template <typename T, Device D>
+void ReduceScatter(T const* sbuf, T* rbuf, int rc, Comm const& comm, SyncInfo<D> const& si) {
+    ReduceScatter(sbuf, rbuf, rc, SUM, comm, si);
+}
+
+// SendRecv (mpi.hpp:593-633): send sc entries to `to` while receiving rc from `from`
+template <typename T, Device D>
+void SendRecv(T const* sbuf, int sc, int to, T* rbuf, int rc, int from, Comm const& comm, SyncInfo<D> const& si) {
+    detail::Check(elx_mpi_sendrecv(comm.Handle(), detail::TypeCode<T>::value, detail_::DevCode<D>(), sbuf, sc, to,
+                                   rbuf, rc, from, detail_::StreamOf(si)));
+}
+// in place: buf's count entries go to `to` and are replaced by `from`'s (the
+// outgoing entries are first copied aside, on the SyncInfo's stream on the GPU)
+template <typename T, Device D>
+void SendRecv(T* buf, int count, int to, int from, Comm const& comm, SyncInfo<D> const& si) {
+    if (count <= 0) return;
+    const int dt = detail::TypeCode<T>::value;
+    if (D == Device::CPU) {
+        std::vector<T> tmp(buf, buf + count);
+        SendRecv(static_cast<T const*>(tmp.data()), count, to, buf, count, from, comm, si);
+        return;
+    }
+    void* tmp = nullptr;
+    detail::Check(elx_pool_alloc(&tmp, sizeof(T) * count, detail_::StreamOf(si)));
+    int rc = elx_matrix_copy(dt, ELX_DEVICE_GPU, count, 1, buf, count, tmp, count, detail_::StreamOf(si));
+    if (rc == ELX_OK)
+        rc = elx_mpi_sendrecv(comm.Handle(), dt, ELX_DEVICE_GPU, tmp, count, to, buf, count, from, detail_::StreamOf(si));
+    const std::string err = rc == ELX_OK ? std::string() : std::string(elx_last_error());
+    (void)elx_pool_free(tmp, detail_::StreamOf(si));
+    if (rc != ELX_OK) detail::Check(rc, err);
+}
 }  // namespace mpi
 
 // ---- El::Grid (src/core/Grid.cpp) --------------------------------------------
@@ -431,13 +538,20 @@ public:
         if (!gpu_) return;
         for (const AbstractMatrix<T>* o : others)
             if (o && o->Stream() != master.Stream()) o_.push_back(o->GPUSyncInfo());
-        for (const auto& o : o_) AddSynchronizationPoint(o, m_);
-    }
-    ~LocalFence() {
-        if (gpu_ && !o_.empty()) {
-            AddSynchronizationPoint(m_);
-            for (const auto& o : o_) hydrogen::details::AddSyncPoint(m_, o);
+        for (const auto& o : o_) {
+            if (o.Event()) AddSynchronizationPoint(o, m_);
+            else Synchronize(o);  // no event to record (moved-from shell): drain its stream
         }
+    }
+    // Never throws (a destructor is noexcept): skipped while an exception from
+    // the fenced call unwinds (the stream may hold a sticky error) or when the
+    // master has no event; a failure to record or wait here is dropped, and the
+    // next checked call on the stream reports it.
+    ~LocalFence() {
+        if (!gpu_ || o_.empty() || !m_.Event() || std::uncaught_exceptions() > uncaught_) return;
+        if (elx_event_record(m_.Event(), m_.Stream()) != ELX_OK) return;
+        for (const auto& o : o_)
+            if (o.Stream() != m_.Stream()) (void)elx_stream_wait_event(o.Stream(), m_.Event());
     }
     LocalFence(const LocalFence&) = delete;
     LocalFence& operator=(const LocalFence&) = delete;
@@ -446,6 +560,7 @@ private:
     bool gpu_;
     SyncInfo<Device::GPU> m_;
     std::vector<SyncInfo<Device::GPU>> o_;
+    int uncaught_ = std::uncaught_exceptions();
 };
 }  // namespace detail
 
@@ -461,7 +576,19 @@ public:
     }
     Matrix(Int height, Int width, Int ldim = 0) : Matrix() { Resize(height, width, ldim); }
     Matrix(const Matrix& A) : Matrix() { *this = A; }
-    Matrix(Matrix&& A) noexcept { Swap(A); }
+    // the moved-from matrix keeps a usable SyncInfo (the default stream and
+    // event, as Matrix() gives), so reusing it as an output fences correctly
+    Matrix(Matrix&& A) noexcept {
+        if (D == Device::GPU) {
+            void* s = nullptr;
+            void* e = nullptr;
+            if (elx_default_stream(&s) == ELX_OK && elx_default_event(&e) == ELX_OK) {
+                this->stream_ = s;
+                this->event_ = e;
+            }
+        }
+        Swap(A);
+    }
     ~Matrix() { Release(); }
     Matrix& operator=(const Matrix& A) {  // deep copy (El::Copy of Matrix)
         if (this == &A) return *this;

@@ -131,6 +131,12 @@ int elx_pool_alloc(void** ptr, size_t bytes, void* stream);
 int elx_pool_free(void* ptr, void* stream);
 int elx_pool_trim(size_t bytes_to_keep);
 int elx_pool_stats(size_t* bytes_reserved, size_t* bytes_in_use);
+/* cap on the bytes held in the cache (H_CUB_MAX_CACHED_SIZE, cub.cpp:37-43;
+ * SIZE_MAX = unbounded, the default); lowering it releases cached blocks */
+int elx_pool_set_max_cached(size_t bytes);
+int elx_pool_max_cached(size_t* bytes);
+/* the bin a request of `bytes` is served from (reserved bytes per block) */
+size_t elx_pool_bin_bytes(size_t bytes);
 int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int elx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int elx_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
@@ -319,6 +325,28 @@ int elx_comm_alltoall(elx_comm_t comm, int dtype, const void* send, void* recv,
                       int64_t count, void* stream);
 int elx_comm_sendrecv(elx_comm_t comm, int dtype, const void* send, int dest,
                       void* recv, int src, int64_t count, void* stream);
+/* El::mpi's typed collectives with the buffers' device explicit (what
+ * El::mpi::*(..., SyncInfo<D>) binds; include/El/core/imports/mpi.hpp:593-633
+ * SendRecv, :675-720 Broadcast, :861-930 AllGather, :1006-1075 AllToAll,
+ * :1248-1351 AllReduce, :1361- ReduceScatter).  device = ELX_DEVICE_GPU: device
+ * buffers, enqueued on `stream` (RCCL) or staged (host backend);
+ * ELX_DEVICE_CPU: host buffers, synchronous (staged through device memory on an
+ * RCCL communicator).  op: the El::mpi::Op of the reduction. */
+#define ELX_OP_SUM  0
+#define ELX_OP_PROD 1
+#define ELX_OP_MAX  2
+#define ELX_OP_MIN  3
+int elx_mpi_allgather(elx_comm_t comm, int dtype, int device, const void* send, void* recv, int64_t count,
+                      void* stream);
+int elx_mpi_reduce_scatter(elx_comm_t comm, int dtype, int device, int op, const void* send, void* recv,
+                           int64_t count, void* stream);
+int elx_mpi_allreduce(elx_comm_t comm, int dtype, int device, int op, const void* send, void* recv,
+                      int64_t count, void* stream);
+int elx_mpi_alltoall(elx_comm_t comm, int dtype, int device, const void* send, void* recv, int64_t count,
+                     void* stream);
+int elx_mpi_bcast(elx_comm_t comm, int dtype, int device, void* buf, int64_t count, int root, void* stream);
+int elx_mpi_sendrecv(elx_comm_t comm, int dtype, int device, const void* send, int64_t send_count, int dest,
+                     void* recv, int64_t recv_count, int src, void* stream);
 /* cumulative traffic counters of the collectives issued by this process */
 int elx_comm_stats(int64_t* bytes_moved, double* seconds, int64_t* calls);
 int elx_comm_stats_reset(void);

@@ -802,6 +802,175 @@ def raw_coll_worker(rank: int, world: int, port: int):
         raise
 
 
+def mpi_typed_worker(rank: int, world: int, port: int, device: int):
+    """El::mpi's typed collectives with an explicit buffer device (elx_mpi_*,
+    what El.hpp's El::mpi::AllGather / ReduceScatter / AllReduce / AllToAll /
+    Broadcast / SendRecv(..., SyncInfo<D>) bind; imports/mpi.hpp:593-1400):
+    every op (SUM, PROD, MAX, MIN) in f64, f32, f16 and bf16 against a rank-order
+    numpy fold, on the world and on a split.  device = GPU: device buffers (RCCL,
+    or staged through the host backend); device = CPU: host buffers (staged
+    through device memory on an RCCL communicator).  Integer-valued inputs, so
+    every op is exact in every type and every backend's order."""
+    import ctypes
+    import oracle
+    from elemental_amd import _lib as L
+    el, comm = init(rank, world, port)
+    rccl = os.environ.get("ELX_TEST_BACKEND") == "rccl"
+    if device == el.GPU:
+        import torch
+
+        def buf(a):
+            return torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()
+
+        def ptr(b):
+            return ctypes.c_void_p(b.data_ptr())
+
+        def get(b):
+            L.call("elx_device_synchronize")
+            torch.cuda.synchronize()
+            return b.cpu().numpy()
+    else:
+        def buf(a):
+            return np.ascontiguousarray(a).copy()
+
+        def ptr(b):
+            return b.ctypes.data_as(ctypes.c_void_p)
+
+        def get(b):
+            return b
+    fmts = ((el.F64, "f64", np.float64), (el.F32, "f32", np.float32), (el.F16, "f16", np.float16),
+            (el.BF16, "bf16", np.uint16))
+    folds = {0: lambda a, b: b + a, 1: lambda a, b: b * a, 2: np.maximum, 3: np.minimum}
+
+    def enc(x, fmt, npdt):  # exact small integers in the storage format
+        if fmt == "bf16":
+            return oracle.convert(np.asarray(x, dtype=np.float64), "f64", "bf16")
+        return np.asarray(x, dtype=npdt)
+
+    def dec(x, fmt):
+        return oracle.to_f64(x, fmt)
+
+    try:
+        def check(c, tag):
+            p, r = c.size, c.rank
+            n = 7
+            for dt, fmt, npdt in fmts:
+                def vals(q, salt):
+                    i = (np.arange(n * p) * 3 + 5 * q + salt) % 7
+                    if salt % 10 == 1:  # PROD: signed powers of two stay exact in every format
+                        return np.array([-1.0, 1.0, 2.0, 1.0, -2.0, 1.0, 1.0])[i]
+                    return (i - 3).astype(np.float64)
+                # AllGather
+                mine = buf(enc(vals(r, 1)[:n], fmt, npdt))
+                out = buf(enc(np.zeros(n * p), fmt, npdt))
+                L.call("elx_mpi_allgather", c.h, dt, device, ptr(mine), ptr(out), n, None)
+                want = np.concatenate([vals(q, 1)[:n] for q in range(p)])
+                assert np.array_equal(dec(get(out), fmt), want), (tag, fmt, "allgather")
+                for op in (0, 1, 2, 3):
+                    # AllReduce: fold rank 0..p-1 in order (exact on small integers)
+                    send = buf(enc(vals(r, op)[:n], fmt, npdt))
+                    recv = buf(enc(np.zeros(n), fmt, npdt))
+                    L.call("elx_mpi_allreduce", c.h, dt, device, op, ptr(send), ptr(recv), n, None)
+                    acc = vals(0, op)[:n]
+                    for q in range(1, p):
+                        acc = folds[op](acc, vals(q, op)[:n])
+                    assert np.array_equal(dec(get(recv), fmt), acc), (tag, fmt, "allreduce", op)
+                    # in place (send == recv)
+                    io = buf(enc(vals(r, op)[:n], fmt, npdt))
+                    L.call("elx_mpi_allreduce", c.h, dt, device, op, ptr(io), ptr(io), n, None)
+                    assert np.array_equal(dec(get(io), fmt), acc), (tag, fmt, "allreduce in place", op)
+                    # ReduceScatter: my slice of every rank's n*p vector
+                    send = buf(enc(vals(r, op + 10), fmt, npdt))
+                    recv = buf(enc(np.zeros(n), fmt, npdt))
+                    L.call("elx_mpi_reduce_scatter", c.h, dt, device, op, ptr(send), ptr(recv), n, None)
+                    acc = vals(0, op + 10)[r * n:(r + 1) * n]
+                    for q in range(1, p):
+                        acc = folds[op](acc, vals(q, op + 10)[r * n:(r + 1) * n])
+                    assert np.array_equal(dec(get(recv), fmt), acc), (tag, fmt, "reduce_scatter", op)
+                # AllToAll
+                send = buf(enc(np.concatenate([np.full(n, (10 * r + q) % 50) for q in range(p)]), fmt, npdt))
+                recv = buf(enc(np.zeros(n * p), fmt, npdt))
+                L.call("elx_mpi_alltoall", c.h, dt, device, ptr(send), ptr(recv), n, None)
+                want = np.concatenate([np.full(n, (10 * q + r) % 50) for q in range(p)])
+                assert np.array_equal(dec(get(recv), fmt), want), (tag, fmt, "alltoall")
+                # Broadcast from the last rank
+                b = buf(enc(vals(r, 3)[:n], fmt, npdt))
+                L.call("elx_mpi_bcast", c.h, dt, device, ptr(b), n, p - 1, None)
+                assert np.array_equal(dec(get(b), fmt), vals(p - 1, 3)[:n]), (tag, fmt, "bcast")
+                # SendRecv around the ring; unequal counts where the backend allows them
+                rc_ = n if not rccl else n - 2 + ((r - 1) % p) % 3
+                sc_ = n if not rccl else n - 2 + r % 3
+                send = buf(enc(vals(r, 4)[:sc_], fmt, npdt))
+                recv = buf(enc(np.zeros(max(rc_, 1)), fmt, npdt))
+                L.call("elx_mpi_sendrecv", c.h, dt, device, ptr(send), sc_, (r + 1) % p, ptr(recv), rc_,
+                       (r - 1) % p, None)
+                assert np.array_equal(dec(get(recv), fmt)[:rc_], vals((r - 1) % p, 4)[:rc_]), (tag, fmt, "sendrecv")
+            # error mapping: a bad op and a bad root are LogicErrors
+            x = buf(np.zeros(2))
+            for call in (lambda: L.call("elx_mpi_allreduce", c.h, el.F64, device, 9, ptr(x), ptr(x), 2, None),
+                         lambda: L.call("elx_mpi_bcast", c.h, el.F64, device, ptr(x), 2, p, None)):
+                try:
+                    call()
+                    raise AssertionError("expected a LogicError")
+                except L.LogicError:
+                    pass
+
+        check(comm, "world")
+        if world > 1:
+            sub = comm.split(rank % 2, rank)
+            check(sub, "split")
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def frobenius_worker(rank: int, world: int, port: int, height: int, device: int):
+    """El::FrobeniusNorm (src/lapack_like/props/Norm/Frobenius.cpp:20-60) of
+    DistMatrices against numpy's norm of the same global values: f64, f32, f16,
+    bf16; ragged shapes wider than 128 columns; [MC,MR], the replicated
+    [STAR,STAR] and [MC,STAR] (each entry counted once), [VC,STAR]; a NaN
+    anywhere gives NaN, an inf gives inf, values near the f64 overflow
+    threshold stay finite (the scaled sum of squares)."""
+    import oracle
+    el, comm = init(rank, world, port)
+    try:
+        g = el.Grid(comm, height)
+        r, c = g.height, g.width
+        dists = [(el.MC, el.MR), (el.STAR, el.STAR), (el.MC, el.STAR), (el.VC, el.STAR)]
+        for dt in (el.F64, el.F32, el.F16, el.BF16):
+            fmt, npdt = W_FMT[dt], _host_dt(dt)
+            rtol = 1e-13 if dt == el.F64 else 1e-6
+            for (m, n) in ((37, 300), (130, 129), (1, 517), (0, 5)):
+                Xg = oracle.hash_matrix(m, n, 17 + m, -1.0, 3.0, npdt)
+                want = float(np.linalg.norm(oracle.to_f64(Xg, fmt))) if Xg.size else 0.0
+                for (U, V) in dists:
+                    X = el.DistMatrix(g, dt, U, V, device, height=m, width=n)
+                    X.set_local(oracle.local_block(Xg, U, V, r, c, g.vc_rank))
+                    got = el.FrobeniusNorm(X)
+                    assert abs(got - want) <= rtol * max(want, 1e-300), (fmt, m, n, U, V, got, want)
+        # special values (f64 and f32 only: the 16-bit hash has no large range)
+        for dt, big in ((el.F64, 1e300), (el.F32, 3e37)):
+            npdt = _host_dt(dt)
+            m, n = 20, 140
+            base = np.asfortranarray(np.full((m, n), big, dtype=npdt))
+            X = el.DistMatrix(g, dt, el.MC, el.MR, device, height=m, width=n)
+            X.set_local(oracle.local_block(base, el.MC, el.MR, r, c, g.vc_rank))
+            got = el.FrobeniusNorm(X)
+            want = float(big) * np.sqrt(m * n)
+            assert np.isfinite(got) and abs(got - want) <= 1e-6 * want, (dt, got, want)
+            for bad, check in ((np.nan, np.isnan), (np.inf, np.isposinf)):
+                Y = base.copy()
+                Y[7, 133] = bad
+                X.set_local(oracle.local_block(Y, el.MC, el.MR, r, c, g.vc_rank))
+                got = el.FrobeniusNorm(X)
+                assert check(got), (dt, bad, got)
+        finish()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
 # tests/golden/mkl_summa.npz cases: dtype_grid_nb_mxnxk
 # tests/golden/mkl_summa_orient.npz: NT / TN / TT through SUMMA_C, TN / NN through SUMMA_DOT
 MKL_ORIENT = [f"{t}_{g}_{o}_C" for t in ("f64", "f32")

@@ -338,6 +338,62 @@ int main() {
         El::Synchronize(si);
         EXPECT(si == El::SyncInfoFromMatrix(Mx));
     }
+    // El::mpi typed collectives on SyncInfo-tagged buffers over COMM_WORLD and
+    // COMM_SELF (imports/mpi.hpp:593-1400): buffers of the test's device
+    {
+        const int n = 6;
+        const auto& comm = El::mpi::COMM_WORLD;
+        const int p = El::mpi::Size(comm), me = El::mpi::Rank(comm);
+        El::Matrix<double, kDev> S(n, 1), R(n * p, 1), T(n, 1);
+        auto si = El::SyncInfoFromMatrix(S);
+        for (int i = 0; i < n; ++i) S.Set(i, 0, 10.0 * me + i - 2.0);
+        El::mpi::AllGather(S.LockedBuffer(), n, R.Buffer(), n, comm, si);
+        bool ok = true;
+        for (int q = 0; q < p; ++q)
+            for (int i = 0; i < n; ++i) ok &= R.Get(q * n + i, 0) == 10.0 * q + i - 2.0;
+        EXPECT(ok);
+        El::mpi::AllReduce(S.LockedBuffer(), T.Buffer(), n, El::mpi::MAX, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == 10.0 * (p - 1) + i - 2.0);
+        El::mpi::AllReduce(T.Buffer(), n, comm, si);  // in place, SUM
+        for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == p * (10.0 * (p - 1) + i - 2.0));
+        El::mpi::AllReduce(S.LockedBuffer(), T.Buffer(), n, El::mpi::MIN, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == i - 2.0);
+        EXPECT(El::mpi::AllReduce(3.0, El::mpi::PROD, comm, si) == std::pow(3.0, p));
+        EXPECT(El::mpi::AllReduce(2.5, comm, si) == 2.5 * p);
+        El::Matrix<double, kDev> RS(n * p, 1), Ro(n, 1);
+        for (int i = 0; i < n * p; ++i) RS.Set(i, 0, i + 1.0);
+        El::mpi::ReduceScatter(RS.LockedBuffer(), Ro.Buffer(), n, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(Ro.Get(i, 0) == p * (me * n + i + 1.0));
+        El::mpi::ReduceScatter(RS.LockedBuffer(), Ro.Buffer(), n, El::mpi::MAX, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(Ro.Get(i, 0) == me * n + i + 1.0);
+        El::Matrix<double, kDev> A2(n * p, 1);
+        El::mpi::AllToAll(RS.LockedBuffer(), n, A2.Buffer(), n, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(A2.Get(i, 0) == me * n + i + 1.0);
+        El::Matrix<double, kDev> B(n, 1);
+        for (int i = 0; i < n; ++i) B.Set(i, 0, me == 0 ? 7.0 + i : -1.0);
+        El::mpi::Broadcast(B.Buffer(), n, 0, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(B.Get(i, 0) == 7.0 + i);
+        El::mpi::SendRecv(S.LockedBuffer(), n, (me + 1) % p, T.Buffer(), n, (me + p - 1) % p, comm, si);
+        for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == 10.0 * ((me + p - 1) % p) + i - 2.0);
+        El::mpi::SendRecv(B.Buffer(), n, (me + 1) % p, (me + p - 1) % p, comm, si);  // in place
+        for (int i = 0; i < n; ++i) EXPECT(B.Get(i, 0) == 7.0 + i);
+        double scalar = me == 0 ? 4.25 : 0.0;
+        El::mpi::Broadcast(scalar, 0, comm, El::SyncInfo<El::Device::CPU>{});
+        EXPECT(scalar == 4.25);
+        bool threw_c = false;
+        try { El::mpi::AllGather(S.LockedBuffer(), n, R.Buffer(), n - 1, comm, si); }
+        catch (const El::LogicError&) { threw_c = true; }
+        EXPECT(threw_c);
+        threw_c = false;
+        try { El::mpi::Broadcast(B.Buffer(), n, p, comm, si); }
+        catch (const El::LogicError&) { threw_c = true; }
+        EXPECT(threw_c);
+        // a split-off self communicator works the same way
+        const El::mpi::Comm self = El::mpi::COMM_SELF();
+        El::mpi::AllReduce(S.LockedBuffer(), T.Buffer(), n, El::mpi::SUM, self, si);
+        for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == 10.0 * me + i - 2.0);
+        El::Synchronize(si);
+    }
 #ifdef EL_TEST_GPU
     {
         using GPU = El::SyncInfo<El::Device::GPU>;
@@ -401,6 +457,36 @@ int main() {
         EXPECT(Ds.Get(5, 4) == 4.0);
         El::SetSyncInfo(Ds.Matrix(), dflt);
         EXPECT(Ds.Stream() == static_cast<void*>(dflt.Stream()));
+
+        // a moved-from matrix keeps a usable SyncInfo and serves as an output
+        // fenced against operands on another stream (LocalFence records on it)
+        {
+            El::Matrix<double, El::Device::GPU> Src(8, 8);
+            El::Fill(Src, 1.0);
+            El::Matrix<double, El::Device::GPU> Dst(std::move(Src));
+            EXPECT(Src.GetSyncInfo().Event() != nullptr && Src.GetSyncInfo().Stream() != nullptr);
+            El::Matrix<double, El::Device::GPU> Qv;
+            Qv.LockedAttach(8, 8, Q.LockedBuffer(), Q.LDim());
+            El::SetSyncInfo(Qv, si1);
+            El::Gemm(El::NORMAL, El::NORMAL, 1.0, Dst, Qv, Src);  // beta-less: Src resized, = 8 * 0.5
+            El::Synchronize(El::SyncInfoFromMatrix(Src));
+            EXPECT(Src.Height() == 8 && Src.Get(0, 0) == 4.0 && Src.Get(7, 7) == 4.0);
+        }
+        {
+            // the fenced call throws after the fence is set up (a locked output)
+            // with operands on another stream: a catchable LogicError, not a
+            // terminate from the fence's destructor
+            El::Matrix<double, El::Device::GPU> Cw(8, 8), Qv, Cl;
+            El::SetSyncInfo(Cw, si2);
+            Qv.LockedAttach(8, 8, Q.LockedBuffer(), Q.LDim());
+            El::SetSyncInfo(Qv, si1);
+            Cl.LockedAttach(8, 8, Cw.LockedBuffer(), Cw.LDim());
+            El::SetSyncInfo(Cl, si2);
+            bool threw_f = false;
+            try { El::Gemm(El::NORMAL, El::NORMAL, 1.0, Qv, Qv, 0.0, Cl); }
+            catch (const El::LogicError&) { threw_f = true; }
+            EXPECT(threw_f);
+        }
 
         for (auto* M : {&P, &Q, &X, &Yh, &Cg}) El::SetSyncInfo(*M, dflt);
         El::Synchronize(dflt);

@@ -119,6 +119,20 @@ def test_raw_collectives(world):
     _spawn(W.raw_coll_worker, world)
 
 
+@pytest.mark.parametrize("world,height", [(1, 1), (2, 2), (4, 2)])
+def test_frobenius_norm(world, height):
+    """El::FrobeniusNorm over distributions, types, replication and specials."""
+    _spawn(W.frobenius_worker, world, height, el.CPU)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_mpi_typed_collectives(world):
+    """elx_mpi_* (El.hpp's El::mpi::AllGather / ReduceScatter / AllReduce /
+    AllToAll / Broadcast / SendRecv on SyncInfo<Device::CPU>): SUM, PROD, MAX,
+    MIN in every element type, host buffers, world and split."""
+    _spawn(W.mpi_typed_worker, world, el.CPU)
+
+
 @pytest.mark.parametrize("world,height,cols", [(1, 1, 0), (2, 1, 0), (4, 2, 0), (1, 1, 3), (4, 2, 2), (2, 2, 5)])
 def test_syrk_herk(world, height, cols, monkeypatch):
     """El::Syrk / El::Herk LN/LT/UN/UT on 1x1, 1x2, 2x1 and 2x2 grids (Syrk/*.hpp);

@@ -83,6 +83,41 @@ def test_rendezvous_bcast(world):
     assert sorted(o[0].strip() for o in outs) == [f"rank {r} ok" for r in range(world)]
 
 
+def test_rendezvous_ignores_stray_connections():
+    """Stray connections to rank 0 (silent, garbage, a wrong world size, a
+    duplicate rank) never use up a peer's slot: both real peers still get the
+    id, and the strays get nothing."""
+    import socket as so
+    port = _port()
+    root = subprocess.Popen([sys.executable, WORKER, "rendezvous", "0", "3", str(port)],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    strays = []
+    deadline = time.monotonic() + 30
+    while not strays:
+        try:
+            strays.append(so.create_connection(("127.0.0.1", port), timeout=2))
+        except OSError:
+            assert time.monotonic() < deadline
+            time.sleep(0.05)
+    import struct
+    for payload in (b"GET / HTTP/1.0\r\n\r\n", b"ELXRDV01" + struct.pack("<ii", 1, 7),
+                    b"ELXRDV01" + struct.pack("<ii", 0, 3), b"ELXRDV01" + struct.pack("<ii", 5, 3)):
+        c = so.create_connection(("127.0.0.1", port), timeout=2)
+        c.sendall(payload)
+        strays.append(c)
+    peers = [subprocess.Popen([sys.executable, WORKER, "rendezvous", str(r), "3", str(port)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (1, 2)]
+    outs = [p.communicate(timeout=60) for p in [root] + peers]
+    assert all(p.returncode == 0 for p in [root] + peers), [o[1] for o in outs]
+    for c in strays:
+        c.settimeout(2)
+        try:
+            assert c.recv(16) == b""  # closed without the payload
+        except (so.timeout, ConnectionResetError):
+            pass
+        c.close()
+
+
 def test_rendezvous_times_out_without_rank0():
     from elemental_amd import el
     from elemental_amd import _lib as L
@@ -92,27 +127,32 @@ def test_rendezvous_times_out_without_rank0():
 
 def test_blocksize_stack_and_comm_world():
     """PushBlocksizeStack / PopBlocksizeStack / EmptyBlocksizeStack
-    (environment/decl.hpp:88-94) and COMM_WORLD (size 1 without a launcher)."""
+    (environment/decl.hpp:88-94) and COMM_WORLD (size 1 without a launcher).
+    The global stack is restored in `finally`, so a failing assertion here
+    cannot leave later tests with an empty stack."""
     from elemental_amd import el
     from elemental_amd import _lib as L
     el.Initialize()
-    assert el.Blocksize() == 128
-    el.PushBlocksizeStack(64)
-    assert el.Blocksize() == 64
-    el.SetBlocksize(32)
-    assert el.Blocksize() == 32
-    el.PopBlocksizeStack()
-    assert el.Blocksize() == 128
-    el.EmptyBlocksizeStack()
-    with pytest.raises(L.LogicError, match="empty stack"):
-        el.Blocksize()
-    with pytest.raises(L.LogicError, match="empty"):
+    try:
+        assert el.Blocksize() == 128
+        el.PushBlocksizeStack(64)
+        assert el.Blocksize() == 64
+        el.SetBlocksize(32)
+        assert el.Blocksize() == 32
         el.PopBlocksizeStack()
-    el.PushBlocksizeStack(128)
-    w = el.Comm.world()
-    assert w.size == 1 and w.rank == 0
-    g = el.Grid(w)
-    assert (g.height, g.width) == (1, 1)
-    el.Finalize()
-    el.PushBlocksizeStack(128)  # Finalize empties the stack; later tests expect the default
+        assert el.Blocksize() == 128
+        el.EmptyBlocksizeStack()
+        with pytest.raises(L.LogicError, match="empty stack"):
+            el.Blocksize()
+        with pytest.raises(L.LogicError, match="empty"):
+            el.PopBlocksizeStack()
+        el.PushBlocksizeStack(128)
+        w = el.Comm.world()
+        assert w.size == 1 and w.rank == 0
+        g = el.Grid(w)
+        assert (g.height, g.width) == (1, 1)
+    finally:
+        el.Finalize()
+        el.EmptyBlocksizeStack()
+        el.PushBlocksizeStack(128)  # Finalize empties the stack; later tests expect the default
     assert el.Blocksize() == 128

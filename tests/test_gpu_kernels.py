@@ -438,11 +438,13 @@ def test_fill_hash_bit_exact(t, npdt):
 
 
 def test_pool_alloc_free():
-    """The hipMallocAsync pool that replaces hipCUB's CachingDeviceAllocator
-    (src/core/imports/cub.cpp): stream-ordered alloc/free, reuse of freed blocks
-    (the reserved size does not grow on a repeat of the same pattern), blocks
-    freed on one stream and reallocated on another, in-use back to zero, and a
-    trim that returns the cached memory."""
+    """The caching allocator that replaces hipCUB's CachingDeviceAllocator
+    (src/core/imports/cub.cpp; contract in csrc/runtime/runtime.hpp):
+    stream-ordered alloc/free, blocks freed on one stream and reallocated on
+    another, in-use back to zero, and the steady-state rule: after one warm-up
+    pass a repeated pattern reserves nothing new, whichever streams it uses.
+    Reserved bytes are the allocator's own bin accounting (live + cached), so
+    the check does not depend on the driver's pool."""
     el.device_synchronize()
     _, u0 = el.pool_stats()
     s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
@@ -464,28 +466,63 @@ def test_pool_alloc_free():
                 L.call("elx_fill2d", L.F32, b // 4, 1, 1.0, p, max(b // 4, 1), alloc_stream)
             for p in ptrs:
                 L.call("elx_pool_free", p, free_stream)
-            L.call("elx_stream_synchronize", free_stream)
             _, u = el.pool_stats()
             assert u == u0
 
         round_trip(s1, s1)
-        round_trip(s2, s1)
-        round_trip(s1, s2)
         r1, _ = el.pool_stats()
-        for _ in range(3):  # freed on s1, reallocated on s2 and back: served from the cache
+        for _ in range(4):  # freed on one stream, reallocated on the other: served from the cache
             round_trip(s2, s1)
             round_trip(s1, s2)
+            round_trip(None, s2)
         r2, _ = el.pool_stats()
-        assert r2 <= r1, (r1, r2)  # nothing new reserved (the driver may release idle pages)
+        assert r2 == r1, (r1, r2)
+        L.call("elx_stream_synchronize", s1)
+        L.call("elx_stream_synchronize", s2)
         L.call("elx_pool_trim", 0)
-        r3, _ = el.pool_stats()
-        assert r3 <= r2
+        r3, u3 = el.pool_stats()
+        assert r3 <= r2 and r3 - u3 <= r2 - u0
         with pytest.raises(L.LogicError, match="not from this pool"):
             L.call("elx_pool_free", ctypes.c_void_p(0x1000), None)
     finally:
         el.device_synchronize()
         L.call("elx_stream_destroy", s1)
         L.call("elx_stream_destroy", s2)
+
+
+def test_pool_bins_and_cap():
+    """Bins (powers of two to 1 MiB, then 8 per octave, >= 2 MiB apart) and the
+    H_CUB_MAX_CACHED_SIZE cap (cub.cpp:37-43): a free past the cap returns the
+    block instead of caching it, so reserved - in_use never exceeds the cap."""
+    lib = L.lib()
+    assert lib.elx_pool_bin_bytes(1) == 512
+    assert lib.elx_pool_bin_bytes(5000) == 8192
+    assert lib.elx_pool_bin_bytes(1 << 20) == 1 << 20
+    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == 2 << 20
+    assert lib.elx_pool_bin_bytes(3 << 20) == 4 << 20
+    for b in [(1 << 30) + 1, 5 << 30, (1 << 33) + 12345, 32 << 30]:
+        bb = lib.elx_pool_bin_bytes(b)
+        assert b <= bb <= b * 1.125 + (2 << 20)
+    el.device_synchronize()
+    old = ctypes.c_size_t()
+    L.call("elx_pool_max_cached", ctypes.byref(old))
+    try:
+        cap = 8 << 20
+        L.call("elx_pool_set_max_cached", cap)
+        r, u = el.pool_stats()
+        assert r - u <= cap
+        ptrs = []
+        for _ in range(6):
+            p = ctypes.c_void_p()
+            L.call("elx_pool_alloc", ctypes.byref(p), 3 << 20, None)
+            ptrs.append(p)
+        for p in ptrs:
+            L.call("elx_pool_free", p, None)
+        r, u = el.pool_stats()
+        assert r - u <= cap, (r, u)
+    finally:
+        L.call("elx_pool_set_max_cached", old.value)
+        el.device_synchronize()
 
 
 @pytest.mark.parametrize("s", [L.F64, L.F32, L.F16, L.BF16])
