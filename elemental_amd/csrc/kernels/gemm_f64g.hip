@@ -34,13 +34,11 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BN = 128, BK = 16, GROUP_M = 8;
-// Tile shapes: BM = 128 (two workgroups per CU) or 256 (one workgroup per CU,
-// 25 % fewer staged bytes per FLOP); wave tiles WTM x 64 with WTM = 32 (2 x 4
-// accumulators, 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read
-// per MFMA, half the waves).  Slab depth SK = 16 (two 32-KiB stages: two
-// workgroups per CU) or 32 (two 64-KiB stages: one workgroup per CU, for grids
-// that have at most one workgroup per CU anyway: twice the MFMAs between
-// barriers, half the barriers and DMA waits).
+// Tile shape: BM = 128 rows, slab depth SK = 16 (two 32-KiB stages: two
+// workgroups per CU); wave tiles WTM x 64 with WTM = 32 (2 x 4 accumulators,
+// 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read per MFMA, half
+// the waves).  (The template also admits BM = 256 and SK = 32, both measured
+// slower and no longer launched.)
 template <int BM_, int WTM_ = 32, int SK_ = BK>
 struct Shape {
     static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW, SK = SK_;
@@ -150,13 +148,10 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
     }
 }
 
-// FL: diagnostic flags (1 = no staging after the first slab, 2 = no slab barrier:
-// timing ablations with wrong results; 4 = static s_setprio 1 for waves 4-7;
-// 8 = no wait for the DMA before the barrier, also wrong results).
 // BUF: stage through buffer descriptors (default where every lane offset of a
 // slab image fits the descriptor's 31-bit range): +2.5 % over global_load_lds
 // (profiles/r01_f64_buf.log).
-template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF, int FL = 0>
+template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF>
 __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GParams p) {
     constexpr int BM = SH::BM, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
@@ -187,20 +182,12 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     stage_img<BUF, KCB, BN, SH::NW, SH::SK>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (FL & 4) {
-        if (w >= SH::NW / 2) __builtin_amdgcn_s_setprio(1);
-    }
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * SH::SK, !(FL & 1) && t + 1 < nt, lds + (cur ^ 1) * STAGE,
-                                lds + cur * STAGE, acc);
-        if (FL & 8) {  // raw barrier: no vmcnt drain (ablation only)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
-            if (!(FL & 2)) __syncthreads();                     // and every wave is done with this one
-        }
+        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * SH::SK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE,
+                                acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next slab landed
+        __syncthreads();                                    // and every wave is done with this one
     }
 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
@@ -255,13 +242,6 @@ hipError_t launch(K kernel, dim3 grid, int nt, const GParams& p, hipStream_t s) 
 
 template <typename SH, bool KCA, bool KCB, bool BUF>
 hipError_t launch_b(const GParams& p, dim3 grid, hipStream_t s) {
-    static const int fl = [] { const char* v = getenv("ELX_F64G_FLAGS"); return v ? atoi(v) : 0; }();
-    if constexpr (!KCA && KCB) {  // timing ablations (NN, beta != 0 form)
-        if (fl == 1) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 1>, grid, SH::NT, p, s);
-        if (fl == 2) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 2>, grid, SH::NT, p, s);
-        if (fl == 4) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 4>, grid, SH::NT, p, s);
-        if (fl == 8) return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF, 8>, grid, SH::NT, p, s);
-    }
     if (p.beta == 0.0) return launch(gemm_f64g_kernel<SH, KCA, KCB, true, BUF>, grid, SH::NT, p, s);
     return launch(gemm_f64g_kernel<SH, KCA, KCB, false, BUF>, grid, SH::NT, p, s);
 }
@@ -305,34 +285,17 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     }();
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
     GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), kchunk, m * n, gm, rm};
-    static const int bm = [] { const char* v = getenv("ELX_F64G_BM"); return v ? atoi(v) : 128; }();
     // wave tile: 64 x 64 (four waves) measured +1.5-2 % for NN/TN/TT; NT (both
     // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();
     // and with at most one workgroup per CU (a grid of <= 256 tiles x chunks) the
     // eight-wave 32 x 64 split keeps two waves per SIMD: 2048^3 NN 61.0 -> 64.0 TF
-    // (4096^3 and up: the four-wave split stays ahead; profiles/r03_f64_small.log)
+    // (4096^3 and up: the four-wave split stays ahead; profiles/r03_f64_small.log).
+    // (Measured and removed in round 4: 256-row tiles, 68.6-72.6 vs 74.1 TF at
+    // 16384^3; 32-deep slabs for one-workgroup-per-CU grids, 53.8 vs 60.6 TF at
+    // 2048^3, profiles/r03_f64_small.log.)
     const i64 grid_wgs = (i64)((m + 127) / 128) * p.tiles_n * ((kmain + kchunk - 1) / kchunk);
     const int wtm = wtm_env ? wtm_env : ((!ta && tb) || grid_wgs <= 256) ? 32 : 64;
-    // ELX_F64G_DEEP=1: grids of at most one workgroup per CU (no split-k) take the
-    // 32-deep slabs on the first kmain/32*32 of k, an odd 16 through the 16-deep
-    // kernel (beta = 1).  Off by default: 2048^3 NN 53.8 vs 60.6 TF with the
-    // 16-deep kernel at one workgroup per CU (profiles/r03_f64_small.log).
-    static const bool deep_few = [] { const char* v = getenv("ELX_F64G_DEEP"); return v && v[0] == '1'; }();
-    const i64 tiles = (i64)((m + 127) / 128) * p.tiles_n;
-    if (deep_few && bm == 128 && kchunk == kmain && tiles <= 256 && kmain >= 32) {
-        GParams q = p;
-        q.k = q.kchunk = kmain / 32 * 32;
-        hipError_t e = wtm == 64 ? launch_shape<Shape<128, 64, 32>>(ta, !tb, q, s) : launch_shape<Shape<128, 32, 32>>(ta, !tb, q, s);
-        if (e != hipSuccess || q.k == kmain) return e;
-        q.A = ta ? A + q.k : A + q.k * lda;
-        q.B = tb ? B + q.k * ldb : B + q.k;
-        q.k = q.kchunk = kmain - q.k;
-        q.alpha = alpha;
-        q.beta = 1.0;
-        return wtm == 64 ? launch_shape<Shape<128, 64>>(ta, !tb, q, s) : launch_shape<Shape<128>>(ta, !tb, q, s);
-    }
-    if (bm == 256) return wtm == 64 ? launch_shape<Shape<256, 64>>(ta, !tb, p, s) : launch_shape<Shape<256>>(ta, !tb, p, s);
     if (wtm == 64) return launch_shape<Shape<128, 64>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);
 }

@@ -1,0 +1,475 @@
+// 16-bit local GEMM, large-tile path for gfx950: C := alpha op(A) op(B) + beta C
+// (column-major, f32 accumulation, bf16 or f16 storage).
+//
+// Replaces rocblas_hgemm on the hot path (src/hydrogen/device/rocBLAS_API.cpp:151-170
+// via include/hydrogen/blas/GPU_BLAS_impl.hpp:397-423, LocalGemm at
+// src/blas_like/level3/Gemm.cpp:163-186) for the shapes SUMMA produces (config
+// C5: local 16384 x 8192 x kc panels).  Edges it does not take (k tail, small or
+// oddly aligned operands) go to the simple kernel of gemm_half.hip.
+//
+// Design (MI355X-first; cdna_hip_programming.md §5 "Canonical CDNA GEMM"):
+//  * 256 x 256 output tile per 256-thread workgroup: four waves (2 x 2), one
+//    per SIMD, each 128 x 128 = 8 x 8 accumulators of
+//    v_mfma_f32_16x16x32_{bf16,f16}; BK = 64 per K-tile, one workgroup per CU.
+//  * Operands are staged HBM -> LDS with LDS DMA (buffer_load ... lds, 16 B per
+//    lane, no VGPR round trip) into a five-slot ring (below).
+//  * Every orientation reads through the same two LDS image kinds:
+//      KC (k contiguous in HBM: op(A) = A^T, op(B) = B): rows of 64 k = 128 B,
+//         read with ds_read_b128 straight into the MFMA fragment;
+//      RC (rows contiguous: op(A) = A, op(B) = B^T): k-rows of 128 elements
+//         = 256 B, read with the gfx950 transposing ds_read_b64_tr_b16 (two
+//         per fragment), so no transpose pass and no extra HBM traffic.
+//    Both images are XOR-swizzled on the 16-B chunk index so the fragment
+//    reads are bank-conflict-free; the swizzle is applied to the GLOBAL source
+//    address of each DMA lane (the LDS side of the DMA is lane-linear).
+//  * XCD-aware bijective workgroup remap with grouped tile order (tile_of).
+// History: the round-1/2 eight-wave kernels (two-stage, phased, balanced-read,
+// deep-prefetch) lived here behind ELX_H16_KERNEL until round 4; their
+// measurements are in profiles/r01_gemm16_h256.log, r01_h16_ablation.log,
+// r02_h16_deep.log and r03_h16_four_wave.log (the four-wave kernel beat each).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdlib>
+#include <utility>
+#include "kernels.hpp"
+#include "lds_dma.hpp"
+#include "elem.hpp"
+
+namespace elx {
+namespace kern {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HALF = 128 * BK * 2;  // one half image: 128 rows x 64 k x 2 B = 16 KiB
+
+struct H2Params {
+    i64 m, n, k;  // k: multiple of BK
+    float alpha, beta;
+    const uint16_t* A; i64 lda;
+    const uint16_t* B; i64 ldb;
+    uint16_t* C; i64 ldc;
+    int tiles_m, tiles_n;
+    int vec_c;    // C base 8-B aligned and ldc % 4 == 0
+    int group_m;  // tile-order group height (ELX_H16_GROUP, default 4)
+};
+
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int per_group = group_m * tiles_n;
+    const int group = wg / per_group;
+    const int first_m = group * group_m;
+    const int gsz = min(tiles_m - first_m, group_m);
+    const int inner = wg - group * per_group;
+    tm = first_m + inner % gsz;
+    tn = inner / gsz;
+}
+
+// XOR swizzles (16-B chunk index).  KC: 8 chunks per 128-B row, row r -> c ^ ((r>>1)&7):
+// the 16 lanes of a ds_read_b128 group (rows r..r+15 of one or two k-chunks) land
+// on 16 distinct 16-B bank slots.  RC: 16 chunks per 256-B k-row, k-row kk ->
+// c ^ (2(kk&3) + 8((kk>>3)&1)): the 8 k-rows x 32 B a 32-lane half of a
+// ds_read_b64_tr_b16 touches land on distinct bank slots; XOR values are even,
+// so the two chunks of a 32-B column pair stay adjacent.
+__device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int swz_rc(int kk) { return ((kk & 3) << 1) | (((kk >> 3) & 1) << 3); }
+
+__device__ __forceinline__ void glds16(const uint16_t* src, lds_char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// One MFMA operand fragment (16 operand rows from R0, k-step s of 32):
+// lane l holds X(R0 + (l&15), 32s + 8(l>>4) + j), j = 0..7.
+template <bool KC>
+__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l) {
+    if (KC) {
+        const int row = R0 + (l & 15), c = 4 * s + (l >> 4);
+        return *(const __attribute__((address_space(3))) u32x4*)(img + row * 128 + ((c ^ swz_kc(row)) << 4));
+    } else {
+        const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+        const int c = (R0 >> 3) + (p >> 1);
+        u32x4 out;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = 32 * s + 8 * g + 4 * h + q;
+            const lds_char* a = img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3);
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+            const u32x2 u = __builtin_bit_cast(u32x2, v);
+            out[2 * h] = u[0];
+            out[2 * h + 1] = u[1];
+        }
+        return out;
+    }
+}
+
+__device__ __forceinline__ void bar8() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// One 16 x 16 accumulator tile: rows i..i+15 (4 per lane), column j.
+template <bool BF16>
+__device__ __forceinline__ void epi_one(const H2Params& p, const f32x4 v4, i64 i, i64 j) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    if (j >= p.n || i >= p.m) return;
+    uint16_t* o = p.C + i + j * p.ldc;
+    if (p.vec_c && i + 3 < p.m) {
+        uint2 cv = make_uint2(0, 0);
+        if (p.beta != 0.f) cv = *reinterpret_cast<const uint2*>(o);
+        const uint16_t in[4] = {(uint16_t)(cv.x & 0xffff), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xffff),
+                                (uint16_t)(cv.y >> 16)};
+        uint16_t r16[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = p.alpha * v4[r];
+            if (p.beta != 0.f) v += p.beta * E::load(in[r]);
+            r16[r] = E::store(v);
+        }
+        *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16),
+                                                  (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (i + r >= p.m) break;
+            float v = p.alpha * v4[r];
+            if (p.beta != 0.f) v += p.beta * E::load(o[r]);
+            o[r] = E::store(v);
+        }
+    }
+}
+
+// every tile with compile-time indices (a fold, not a loop: a loop the unroller
+// declines would index the accumulators dynamically and push them to scratch)
+template <bool BF16, int NI, int... Q>
+__device__ __forceinline__ void epilogue_seq(const H2Params& p, const f32x4 (&acc)[8][NI], i64 rb, i64 cb,
+                                             std::integer_sequence<int, Q...>) {
+    (epi_one<BF16>(p, acc[Q / NI][Q % NI], rb + (Q / NI) * 16, cb + (Q % NI) * 16), ...);
+}
+
+template <bool BF16, int NI>
+__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][NI], i64 m0, i64 n0, int wr, int wc,
+                                         int l) {
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * (16 * NI) + (l & 15);
+    epilogue_seq<BF16, NI>(p, acc, rb, cb, std::make_integer_sequence<int, 8 * NI>{});
+}
+
+// Four-wave kernel: a 256 x 256 output tile over 4 waves (2 x 2), one per
+// SIMD, each owning 128 x 128 = 8 x 8 accumulators (256 AGPRs; the wave has the
+// whole 512-entry file).  Per FLOP this halves the B-fragment LDS reads of the
+// eight-wave kernels (a wave's fragments feed 8 x 8 MFMAs instead of 8 x 4), cuts
+// a third of all LDS instructions, and leaves no partner wave on the SIMD to take
+// matrix-pipe slots or issue bandwidth (MI355X_MICROARCH.md "Two waves per SIMD"
+// items 1-3): each wave issues its own fragment reads and staging between its
+// MFMAs.  hipBLASLt's bf16 kernels on these shapes have the same geometry
+// (MT256x256x64, MI16x16, 4 waves: profiles/r03_vendor_pmc.json).
+//
+// Staging unit = one operand's K-tile image (256 rows x 64 k = 32 KiB, the KC /
+// RC images: two 128-row halves of 128-B KC rows or 256-B RC k-rows), in a
+// ring of 5 slots (160 KiB): A_t is unit 2t, B_t unit 2t+1, unit u in slot u % 5.
+// Each K-tile runs as two k-steps of 64 MFMAs per wave:
+//   (t,0): MFMAs on fragments (t,0) [set X]; read fragments (t,1) [set Y] from
+//          A_t, B_t; stage A_{t+2} into B_{t-1}'s slot; then vmcnt(8) (A_{t+1}
+//          and B_{t+1} landed, A_{t+2} may stay in flight), lgkmcnt(0), barrier;
+//   (t,1): MFMAs on (t,1) [Y]; read (t+1,0) [X] from A_{t+1}, B_{t+1}; stage
+//          B_{t+2} into A_t's slot; lgkmcnt(0), no barrier.
+// RAW: A_{t+1}, B_{t+1} are read from (t,1) on, after every wave's wait and the
+// barrier ending (t,0).  WAR: A_t's and B_t's last reads are issued in (t,0) and
+// retired before that barrier; their slots are restaged in (t,1) and (t+1,0).
+// No wave can be two k-steps ahead of another (it would have passed a barrier
+// the other has not reached), so one barrier per K-tile suffices.  Units past
+// the end re-stage the last K-tile into a slot nobody reads again, so every
+// k-step issues the same 8 pieces and the counted wait is exact without branches.
+// The accumulators are tied to AGPRs through inline asm (mfma_acc).
+// ---------------------------------------------------------------------------
+namespace w4 {
+constexpr int UNIT = 256 * BK * 2;  // one operand's K-tile image: 32 KiB
+constexpr int NSLOT = 5;
+
+// per-lane offset (elements from the image's corner at k0) of piece j (0..31)
+// of one operand's K-tile image: half j >> 4, wave-instruction j & 15 of it, as
+// the image is laid out: 16 wave-instructions of 1 KiB per 128-row half
+template <bool KC>
+__device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld) {
+    const int h = j >> 4, ins = j & 15;
+    if (KC) {
+        const int r = ins * 8 + (l >> 3);
+        const int c = (l & 7) ^ swz_kc(r);
+        const i64 row0 = h * 128 + r;
+        const i64 row = R0 + row0 < rows ? row0 : rows - 1 - R0;
+        return row * ld + 8 * c;
+    } else {
+        const int kk = ins * 4 + (l >> 4);
+        const int c = (l & 15) ^ swz_rc(kk);
+        const i64 col0 = h * 128 + 8 * c;
+        const i64 col = R0 + col0 <= rows - 8 ? col0 : rows - 8 - R0;
+        return col + kk * ld;
+    }
+}
+
+template <bool KC>
+__device__ __forceinline__ const uint16_t* tile_base(const uint16_t* X, i64 ld, i64 R0, i64 k0) {
+    return KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
+}
+
+template <bool BUF, bool KC>
+__device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int j,
+                                      lds_char* img) {
+    if constexpr (BUF) {
+        const BufferSrc<uint16_t> src(tile_base<KC>(X, ld, R0, k0), (KC ? 256 : BK) * ld * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + j * 1024), 16,
+                                                 off, 0, 0, 0);
+    } else {
+        glds16(tile_base<KC>(X, ld, R0, k0) + goff, img + j * 1024);
+    }
+}
+
+struct Sets {
+    u32x4 a[8], b[8];
+};
+
+// acc += a b with the accumulator tied to one AGPR quad.  Written as asm: the
+// builtin's accumulators get rotated through fresh registers (earlyclobber form)
+// at 256 live accumulators, costing ~2 v_accvgpr moves per MFMA.  Only other
+// MFMAs of the same accumulator read it inside the loop (accumulate chains need
+// no wait states); the kernel pads before the epilogue's first read (settle).
+template <bool BF16>
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const u32x4& a, const u32x4& b) {
+    if constexpr (BF16) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// 8-pass MFMA result -> any non-MFMA reader: 12 wait states (then the registers
+// are handed to the compiler through empty asm statements ordered after the pad)
+__device__ __forceinline__ void settle(f32x4 (&acc)[8][8]) {
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+}
+
+// C tile of one wave (128 x 128): accumulator (mi, ni) holds rows
+// rb + 16 mi + 4 (l >> 4) + {0..3}, column cb + 16 ni + (l & 15).  One row of
+// accumulators at a time (C loads, then stores), so at most 32 values live in
+// VGPRs; interior tiles with an 8-B-aligned C take the unchecked path.
+template <bool BF16>
+__device__ __forceinline__ void epilogue4(const H2Params& p, const f32x4 (&acc)[8][8], i64 m0, i64 n0, int wr, int wc,
+                                          int l) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 128 + (l & 15);
+    const bool fast = p.vec_c && m0 + BM <= p.m && n0 + BN <= p.n;
+    if (fast) {
+        uint16_t* o0 = p.C + rb + cb * p.ldc;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            uint2 cv[8];
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                cv[ni] = p.beta != 0.f ? *reinterpret_cast<const uint2*>(o0 + mi * 16 + ni * 16 * p.ldc) : make_uint2(0, 0);
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) {
+                const uint16_t in[4] = {(uint16_t)(cv[ni].x & 0xffff), (uint16_t)(cv[ni].x >> 16),
+                                        (uint16_t)(cv[ni].y & 0xffff), (uint16_t)(cv[ni].y >> 16)};
+                uint16_t r16[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = p.alpha * acc[mi][ni][r];
+                    if (p.beta != 0.f) v += p.beta * E::load(in[r]);
+                    r16[r] = E::store(v);
+                }
+                *reinterpret_cast<uint2*>(o0 + mi * 16 + ni * 16 * p.ldc) =
+                    make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16), (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+            }
+        }
+    } else {
+        epilogue<BF16, 8>(p, acc, m0, n0, wr, wc, l);
+    }
+}
+
+struct Pieces {  // this wave's staging pieces w + 4u, u = 0..7, of each operand's image
+    int offA[8], offB[8];
+    i64 gA[8], gB[8];
+};
+
+// One k-step: 64 MFMAs on `cur`, the 16 fragments of k-step `srd` of the K-tile in
+// (rdA, rdB) into `nxt`, and the 8 pieces of one unit (operand SB ? B : A at k0)
+// into `st`.  The LDS pointers are __restrict__ so the inlined accesses carry
+// alias scopes: hipcc's waitcnt pass then knows the in-flight DMA cannot alias
+// the fragment reads (without them it drains vmcnt(0) before every
+// ds_read_b64_tr_b16).
+template <bool BF16, bool KCA, bool KCB, bool BUF, bool SB>
+__device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
+                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
+                                      f32x4 (&acc)[8][8], const Sets& cur, Sets& nxt) {
+    // Placement (measured, profiles/r03_h16_four_wave.log): the 16 fragment reads
+    // of the next k-step go out one per MFMA in the first 16 MFMAs (+1-2 % over
+    // two per 4-MFMA group in groups 0-7), the 8 staging pieces one per 4-MFMA
+    // group in groups 8-15, in both k-steps: a piece issued among the reads costs
+    // more MFMA time than the later landing of B_{t+2} (issued in the second half
+    // of (t,1), read after (t+1,0)) costs in waiting.
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int mi = q >> 1, ni = (q & 1) * 4 + t;
+            mfma_acc<BF16>(acc[mi][ni], cur.a[mi], cur.b[ni]);
+            if (t == 1 && q >= 8) {
+                const int u = q - 8;
+                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+            }
+            const int f = 4 * q + t;  // read f: A fragments 0-7, then B 0-7
+            if (f < 16) {
+                if (f < 8) nxt.a[f] = frag<KCA>(rdA + wr * HALF, f * 16, srd, l);
+                else nxt.b[f - 8] = frag<KCB>(rdB + wc * HALF, (f - 8) * 16, srd, l);
+            }
+        }
+    }
+}
+}  // namespace w4
+
+template <bool BF16, bool KCA, bool KCB, bool BUF>
+__global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
+    using namespace w4;
+    __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
+    lds_char* lds = (lds_char*)lds_raw;
+
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+
+    Pieces pc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.offA[u] = (int)(pc.gA[u] * 2);
+        pc.offB[u] = (int)(pc.gB[u] * 2);
+    }
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / BK);
+    auto kt = [&](int t) { return (i64)min(t, nt - 1) * BK; };
+        // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; fragments (0,0)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar8();
+    Sets X, Y;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        X.a[q] = frag<KCA>(lds + wr * HALF, q * 16, 0, l);
+        X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // One K-tile; J = t % 5 makes every slot a compile-time offset of the LDS
+    // base (the loop is unrolled by the ring length), so the fragment reads and
+    // the DMA destinations need no address arithmetic in the loop.
+    auto ktile = [&](auto jc, int t) {
+        constexpr int J = decltype(jc)::value;
+        constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
+                      sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
+        // (t,0): stage A_{t+2} into B_{t-1}'s slot
+        w4::kstep<BF16, KCA, KCB, BUF, false>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
+                                                 lds + st0 * UNIT, kt(t + 2), acc, X, Y);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar8();
+        // (t,1): stage B_{t+2} into A_t's slot
+        w4::kstep<BF16, KCA, KCB, BUF, true>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+                                                lds + st1 * UNIT, kt(t + 2), acc, Y, X);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int t = 0; t < nt; t += NSLOT) {
+        ktile(std::integral_constant<int, 0>{}, t);
+        if (t + 1 < nt) ktile(std::integral_constant<int, 1>{}, t + 1);
+        if (t + 2 < nt) ktile(std::integral_constant<int, 2>{}, t + 2);
+        if (t + 3 < nt) ktile(std::integral_constant<int, 3>{}, t + 3);
+        if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
+    w4::settle(acc);
+    w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
+}
+
+template <bool BF16, bool KCA, bool KCB>
+hipError_t launch_h16(const H2Params& p, hipStream_t s) {
+    // buffer-descriptor DMA when every offset of an image fits 31 bits, else the
+    // global (64-bit address) form
+    const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
+    if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+// Tile-order group height: 4, so the 32 concurrent tiles of an XCD span 4 x 8
+// tiles (+1-3 % over 8 x 4 at 32768^3 and 16384^3, profiles/r03_h16_four_wave.log);
+// ELX_H16_GROUP overrides (read per call: A/B tools interleave values), clamped
+// to >= 1 because tile_of divides by it.
+int GroupM() {
+    const char* v = getenv("ELX_H16_GROUP");
+    const int g = v ? atoi(v) : 4;
+    return g >= 1 ? g : 1;
+}
+
+}  // namespace
+
+#ifndef ELX_KERNEL_PROBE
+hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
+                       i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
+    const bool kca = ta, kcb = !tb;
+    const i64 kmain = k / BK * BK;
+    // the large-tile path: 16-B aligned rows/columns for the DMA, RC operands a
+    // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
+    const bool ok = kmain > 0 && al16(A) && al16(B) && lda % 8 == 0 && ldb % 8 == 0 &&
+                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) &&
+                    ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 64 && m < (1ll << 31) && n < (1ll << 31);
+    if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
+    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM()};
+    hipError_t e;
+    if (is_bf16) {
+        if (kca) e = kcb ? launch_h16<true, true, true>(p, s) : launch_h16<true, true, false>(p, s);
+        else e = kcb ? launch_h16<true, false, true>(p, s) : launch_h16<true, false, false>(p, s);
+    } else {
+        if (kca) e = kcb ? launch_h16<false, true, true>(p, s) : launch_h16<false, true, false>(p, s);
+        else e = kcb ? launch_h16<false, false, true>(p, s) : launch_h16<false, false, false>(p, s);
+    }
+    if (e != hipSuccess || kmain == k) return e;
+    // k tail (< 64): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
+    const uint16_t* At = ta ? A + kmain : A + kmain * lda;
+    const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
+    return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);
+}
+
+#endif  // ELX_KERNEL_PROBE
+
+}  // namespace kern
+}  // namespace elx

@@ -195,9 +195,6 @@ struct TileCfg {
 };
 using Tile128 = TileCfg<128, 128, 2, 2, 2>;   // 4 waves of 64x64, 2 per SIMD
 using Tile128w8 = TileCfg<128, 128, 4, 2, 2>; // 8 waves of 32x64, 4 per SIMD
-using Tile128w8n = TileCfg<128, 128, 2, 4, 2>;// 8 waves of 64x32, 4 per SIMD
-using Tile128w16 = TileCfg<128, 128, 4, 4, 2>;// 16 waves of 32x32, 8 per SIMD
-using Tile256 = TileCfg<256, 128, 2, 2, 1>;
 using Tile256w8 = TileCfg<256, 128, 4, 2, 1>;  // 8 waves of 64x64, 2 per SIMD, 1 block/CU
 
 template <typename T, typename CFG, bool TA, bool TB, bool BETA0, bool VEC, bool OFF32>
@@ -391,7 +388,7 @@ static hipError_t launch_split(GemmParams<T> p, hipStream_t s) {
     const int nz = (int)((p.k + kchunk - 1) / kchunk);
     T* W = nullptr;
     const size_t bytes = sizeof(T) * (size_t)p.m * (size_t)p.n * (size_t)nz;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&W), bytes, s);
+    hipError_t e = workspace_alloc(reinterpret_cast<void**>(&W), bytes, s);
     if (e != hipSuccess) return e;
     GemmParams<T> q = p;
     q.alpha = T(1);
@@ -402,21 +399,16 @@ static hipError_t launch_split(GemmParams<T> p, hipStream_t s) {
     q.zstride = p.m * p.n;
     e = launch_cfg<T, CFG, TA, TB, VEC, OFF32>(q, s);
     if (e == hipSuccess) e = launch_reduce(p.m, p.n, nz, p.alpha, W, p.beta, p.C, p.ldc, s);
-    const hipError_t f = hipFreeAsync(W, s);
+    const hipError_t f = workspace_free(W, s);
     return e != hipSuccess ? e : f;
 }
 
-// Tile configuration (measured on MI355X, tools/variants.sh, 16384^3 NN):
-//   f64: 128x128 with 8 waves of 32x64 (4 waves per SIMD)   66.1 TF vs 62.9 (4 waves), 62.8 (256x128)
-//   f32: 256x128 with 8 waves of 64x64 (1 block per CU)    127.5 TF vs 124.5 (128x128, 4 waves)
-// ELX_GEMM_TILE = 128 | 1288 | 1289 | 12816 | 256 | 2568 overrides (A/B measurements only).
-template <typename T>
-static int tile_choice() {
-    static const int forced = [] { const char* v = getenv("ELX_GEMM_TILE"); return v ? atoi(v) : 0; }();
-    if (forced) return forced;
-    return sizeof(T) == 8 ? 1288 : 2568;
-}
-
+// Tile configuration of the register-staged kernel (measured on MI355X,
+// 16384^3 NN, profiles/r01_tile_variants.log): f64 128x128 with 8 waves of
+// 32x64 (66.1 TF vs 62.9 with 4 waves, 62.8 at 256x128); f32 256x128 with 8
+// waves of 64x64, one block per CU (127.5 TF vs 124.5 at 128x128).  The
+// LDS-DMA kernels take every shape their plan accepts; this kernel serves the
+// rest (edges, k tails, unaligned operands).
 template <typename T, bool TA, bool TB>
 static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
     // 16-byte loads need 16-byte aligned bases, even leading dimensions and an
@@ -426,40 +418,12 @@ static hipError_t launch_tn(const GemmParams<T>& p, hipStream_t s) {
     const bool b_even = TB ? (p.n % 2 == 0) : (p.k % 2 == 0);
     const bool vec = al(p.A) && al(p.B) && p.lda % 2 == 0 && p.ldb % 2 == 0 && a_even && b_even;
     const bool off32 = vec && p.lda < (1 << 24) && p.ldb < (1 << 24);
-    const int tc = tile_choice<T>();
     if (off32) {
-        switch (tc) {
-        case 256: return launch_split<T, Tile256, TA, TB, true, true>(p, s);
-        case 1288: return launch_split<T, Tile128w8, TA, TB, true, true>(p, s);
-        case 1289: return launch_split<T, Tile128w8n, TA, TB, true, true>(p, s);
-        case 12816: return launch_split<T, Tile128w16, TA, TB, true, true>(p, s);
-        case 2568: return launch_split<T, Tile256w8, TA, TB, true, true>(p, s);
-        default: return launch_split<T, Tile128, TA, TB, true, true>(p, s);
-        }
+        if (sizeof(T) == 8) return launch_split<T, Tile128w8, TA, TB, true, true>(p, s);
+        return launch_split<T, Tile256w8, TA, TB, true, true>(p, s);
     }
     if (vec) return launch_split<T, Tile128, TA, TB, true, false>(p, s);
     return launch_split<T, Tile128, TA, TB, false, false>(p, s);
-}
-
-// fp64 kernel choice: "dma" (default) = gemm_f64g.hip, LDS-DMA staging, 70.9 TF
-// at 16384^3 vs 65.9 for "reg" = the register-staged tile kernel here
-// (tools/f64_ab.py, profiles/r01_f64_ab.log); ELX_F64_KERNEL=reg|dma overrides.
-static bool f64_use_dma() {
-    static const bool dma = [] {
-        const char* v = getenv("ELX_F64_KERNEL");
-        return v ? std::string(v) != "reg" : true;
-    }();
-    return dma;
-}
-
-// fp32 kernel choice: "dma" = gemm_f32g.hip, "reg" = the 256x128 register-staged
-// kernel here; ELX_F32_KERNEL overrides.
-static bool f32_use_dma() {
-    static const bool dma = [] {
-        const char* v = getenv("ELX_F32_KERNEL");
-        return v ? std::string(v) != "reg" : true;
-    }();
-    return dma;
 }
 
 static DmaPlan plan_dma(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B, i64 ldb) {
@@ -480,7 +444,9 @@ static hipError_t run_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk,
 template <typename T>
 hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
                      const T* B, i64 ldb, T beta, T* C, i64 ldc, hipStream_t s) {
-    if (sizeof(T) == 8 ? f64_use_dma() : f32_use_dma()) {
+    {
+        // the LDS-DMA kernels (gemm_f64g.hip / gemm_f32g.hip: 70.9 vs 65.9 TF for
+        // this file's register-staged kernel at f64 16384^3, profiles/r01_f64_ab.log)
         const DmaPlan d = plan_dma(ta, tb, m, n, k, A, lda, B, ldb);
         if (d.use) {
             hipError_t e;
@@ -488,11 +454,11 @@ hipError_t gemm_mfma(bool ta, bool tb, i64 m, i64 n, i64 k, T alpha, const T* A,
                 e = run_dma(ta, tb, m, n, d.kmain, d.kmain, alpha, A, lda, B, ldb, beta, C, ldc, s);
             } else {  // split-k: nz partials into a stream-ordered workspace, then the ordered reduce
                 T* W = nullptr;
-                e = hipMallocAsync(reinterpret_cast<void**>(&W), sizeof(T) * (size_t)m * (size_t)n * d.nz, s);
+                e = workspace_alloc(reinterpret_cast<void**>(&W), sizeof(T) * (size_t)m * (size_t)n * d.nz, s);
                 if (e != hipSuccess) return e;
                 e = run_dma(ta, tb, m, n, d.kmain, d.kchunk, T(1), A, lda, B, ldb, T(0), W, m, s);
                 if (e == hipSuccess) e = launch_reduce(m, n, d.nz, alpha, W, beta, C, ldc, s);
-                const hipError_t f = hipFreeAsync(W, s);
+                const hipError_t f = workspace_free(W, s);
                 if (e == hipSuccess) e = f;
             }
             if (e != hipSuccess || d.kmain == k) return e;

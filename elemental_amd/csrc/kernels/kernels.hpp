@@ -7,6 +7,12 @@
 namespace elx {
 namespace kern {
 
+// Stream-ordered scratch for the launchers (split-k partials): the library's
+// caching allocator (runtime.cpp), never a driver mempool of its own.
+// Returns hipErrorOutOfMemory instead of throwing.
+hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t s);
+hipError_t workspace_free(void* p, hipStream_t s);
+
 using i64 = int64_t;
 
 template <typename T>

@@ -1,4 +1,5 @@
 #include "runtime.hpp"
+#include "../kernels/kernels.hpp"
 #include <algorithm>
 #include <cstdlib>
 #include <limits>
@@ -77,7 +78,13 @@ void Runtime::EnsureGPU() {
     props.location.type = hipMemLocationTypeDevice;
     props.location.id = device_;
     ELX_CHECK_HIP(hipMemPoolCreate(&pool_, &props));
-    uint64_t thresh = 0;  // caching happens in cache_; the backing returns what it is given
+    // The backing pool keeps what it is given back (threshold = max); memory
+    // returns to the driver only in Trim, after a device synchronize.  With a
+    // release threshold of 0 the driver trims at every synchronize, and the
+    // round-4 GPU suite saw stream-ordered reuse of such a pool hand out blocks
+    // whose previous user had not finished (intermittent wrong GEMM results,
+    // gone with the threshold at max as in rounds 1-3).
+    uint64_t thresh = std::numeric_limits<uint64_t>::max();
     ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolAttrReleaseThreshold, &thresh));
     int on = 1;
     ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseFollowEventDependencies, &on));
@@ -146,7 +153,10 @@ void* Runtime::Alloc(size_t bytes, hipStream_t s) {
     const size_t bin = BinBytes(bytes);
     std::lock_guard<std::mutex> lk(mu_);
     void* p = nullptr;
+    // ELX_POOL_CACHE=0 (debug): no caching, every request from the backing pool
+    static const bool nocache = [] { const char* e = std::getenv("ELX_POOL_CACHE"); return e && e[0] == '0'; }();
     auto [lo, hi] = cache_.equal_range(bin);
+    if (nocache) lo = hi;
     if (lo != hi) {
         // prefer a block last used on this stream, then one whose free has
         // completed, then any (ordered behind its free's event)
@@ -169,6 +179,10 @@ void* Runtime::Alloc(size_t bytes, hipStream_t s) {
     live_[p] = Live{bytes, bin};
     in_use_ += bytes;
     live_bin_ += bin;
+    // ELX_POOL_POISON=1 (debug): every block handed out is filled with 0xFF
+    // bytes (NaN in every float type), so a read before the first write shows up
+    static const bool poison = [] { const char* e = std::getenv("ELX_POOL_POISON"); return e && e[0] == '1'; }();
+    if (poison) ELX_CHECK_HIP(hipMemsetAsync(p, 0xFF, bin, s));
     return p;
 }
 
@@ -179,7 +193,8 @@ void Runtime::Free(void* p, hipStream_t s) {
     if (it == live_.end()) throw LogicError("elx_pool_free: pointer not from this pool");
     const Live l = it->second;
     if (!s) s = compute_;
-    if (cached_ + l.bin > max_cached_) {
+    static const bool nocache = [] { const char* e = std::getenv("ELX_POOL_CACHE"); return e && e[0] == '0'; }();
+    if (nocache || cached_ + l.bin > max_cached_) {
         ELX_CHECK_HIP(hipFreeAsync(p, s));  // over the cap: back to the backing pool
     } else {
         hipEvent_t ev = nullptr;
@@ -220,6 +235,26 @@ void Runtime::Stats(size_t& reserved, size_t& in_use) {
     reserved = live_bin_ + cached_;
     in_use = in_use_;
 }
+
+namespace kern {
+hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t s) {
+    try {
+        *p = Runtime::Get().Alloc(bytes, s);
+        return hipSuccess;
+    } catch (...) {
+        *p = nullptr;
+        return hipErrorOutOfMemory;
+    }
+}
+hipError_t workspace_free(void* p, hipStream_t s) {
+    try {
+        Runtime::Get().Free(p, s);
+        return hipSuccess;
+    } catch (...) {
+        return hipErrorInvalidValue;
+    }
+}
+}  // namespace kern
 
 void Buffer::Reset(Device d, size_t bytes, hipStream_t s) {
     Release();

@@ -17,9 +17,12 @@
 //    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE):
 //    a free that would exceed the cap returns the block to the backing pool;
 //  * the backing store is the library's own hipMemPool (hipMemPoolCreate,
-//    release threshold 0), never the device's default pool shared with other
-//    users of the process; a failed backing allocation releases the cache and
-//    retries once before reporting out-of-memory.
+//    release threshold max: memory goes back to the driver only in Trim, after
+//    a device synchronize), never the device's default pool shared with other
+//    users of the process; every device scratch of the library (the split-k
+//    partials too, kern::workspace_alloc) comes from this allocator; a failed
+//    backing allocation releases the cache and retries once before reporting
+//    out-of-memory.
 #pragma once
 #include "../common.hpp"
 #include <map>

@@ -90,10 +90,10 @@ def test_local_gemm_known_answer_exact(k):
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2048, 2072), (2000, 1990, 1056), (1024, 1024, 288)])
 def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
-    """Grids of at most one workgroup per CU (with ELX_F64G_DEEP=1 the 32-deep-slab
-    fp64 kernel, gemm_f64g.hip Shape<128,64,32>, an odd 16 through the 16-deep
-    kernel) and the k % 16 tail through the general one (2072 = 2048 + 16 + 8):
-    integer operands, so every orientation must match exactly."""
+    """Grids of at most one workgroup per CU (the eight-wave 32 x 64 split of the
+    fp64 LDS-DMA kernel) and the k % 16 tail through the general kernel
+    (2072 = 2048 + 16 + 8): integer operands, so every orientation must match
+    exactly."""
     m, n, k = shape
     rng = np.random.default_rng(k)
     A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
