@@ -25,6 +25,13 @@
  * prints one JSON object; inputs are the oracle's hash (Uniform(-0.1, 0.1)),
  * alpha = 0.5, beta = -0.5; 8 entries per rank are checked against direct dot
  * products of the global inputs before the timing is reported.
+ *
+ * Placement (round 4): rank q pins itself to its own THREADS cpus of the
+ * process's allowed set (cpus q*THREADS .. q*THREADS+THREADS-1 of it) before
+ * MKL's OpenMP runtime starts, and its threads spin between the per-panel
+ * calls (OMP_WAIT_POLICY=ACTIVE: the cpus are the rank's alone), as an MPI
+ * launcher's --bind-to core placement runs the reference.  CPU_SUMMA_PIN=0
+ * keeps the unpinned, passive-wait placement of rounds 2-3.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -34,6 +41,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/wait.h>
 #include <time.h>
@@ -132,8 +140,25 @@ static void one_step(struct Rank* R) {
     }
 }
 
+static int pin_ranks(void) {
+    const char* e = getenv("CPU_SUMMA_PIN");
+    return !(e && e[0] == '0');
+}
+
 static int run_rank(int rank, int n, int nb, int r, int c, int threads, double seconds, const char* mkl_path,
                     struct Shared* sh, double* slots, size_t slot_elems) {
+    if (pin_ranks()) {  /* this rank's own cpus (see the header) */
+        cpu_set_t all, mine;
+        CPU_ZERO(&mine);
+        if (sched_getaffinity(0, sizeof(all), &all) == 0) {
+            int seen = 0, got = 0;
+            for (int cpu = 0; cpu < CPU_SETSIZE && got < threads; ++cpu) {
+                if (!CPU_ISSET(cpu, &all)) continue;
+                if (seen++ >= rank * threads) { CPU_SET(cpu, &mine); ++got; }
+            }
+            if (got == threads) sched_setaffinity(0, sizeof(mine), &mine);
+        }
+    }
     struct Rank R = {0};
     R.rank = rank; R.n = n; R.nb = nb; R.r = r; R.c = c; R.world = r * c; R.threads = threads;
     R.mc = rank % r; R.mr = rank / r;
@@ -221,7 +246,8 @@ int main(int argc, char** argv) {
     pthread_barrierattr_setpshared(&ba, PTHREAD_PROCESS_SHARED);
     pthread_barrier_init(&sh->bar, &ba, (unsigned)world);
     setenv("MKL_THREADING_LAYER", "GNU", 1); /* the reference's runs require GNU or SEQUENTIAL */
-    if (!getenv("OMP_WAIT_POLICY")) setenv("OMP_WAIT_POLICY", "PASSIVE", 1);
+    if (!getenv("OMP_WAIT_POLICY")) setenv("OMP_WAIT_POLICY", pin_ranks() ? "ACTIVE" : "PASSIVE", 1);
+    if (!getenv("MKL_DYNAMIC")) setenv("MKL_DYNAMIC", "FALSE", 1);  /* exactly THREADS threads per call */
     pid_t pids[64];
     for (int q = 0; q < world; ++q) {
         pids[q] = fork();

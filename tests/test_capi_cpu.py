@@ -73,6 +73,29 @@ def test_gpu_matrix_without_device_fails_loudly():
         L.call("elx_gemm_f64", 0, 0, 1, 1, 1, 1.0, None, 1, None, 1, 0.0, None, 1, None)
 
 
+def test_pool_bins_and_cap_setting_without_device():
+    """The caching allocator's bin rule (powers of two to 1 MiB, then eight bins
+    per octave with a 2 MiB floor: runtime.hpp's contract) and its cap setting
+    (H_CUB_MAX_CACHED_SIZE, cub.cpp:37-43) need no device."""
+    lib = L.lib()
+    assert [lib.elx_pool_bin_bytes(b) for b in (0, 1, 512, 513, 5000, 1 << 20)] == [512, 512, 512, 1024, 8192, 1 << 20]
+    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == 2 << 20
+    prev = 0
+    for b in [(3 << 20) + 7, 100 << 20, (1 << 30) + 1, 5 << 30, 32 << 30, (1 << 35) + 3]:
+        bb = lib.elx_pool_bin_bytes(b)
+        assert b <= bb <= b * 1.125 + (2 << 20) and bb % (2 << 20) == 0 and bb > prev
+        prev = bb
+    old = L.ctypes.c_size_t()
+    L.call("elx_pool_max_cached", L.ctypes.byref(old))
+    try:
+        L.call("elx_pool_set_max_cached", 123 << 20)
+        v = L.ctypes.c_size_t()
+        L.call("elx_pool_max_cached", L.ctypes.byref(v))
+        assert v.value == 123 << 20
+    finally:
+        L.call("elx_pool_set_max_cached", old.value)
+
+
 def test_cpu_matrices_local_gemm_and_redistribution():
     g = el.Grid()
     import oracle

@@ -1,11 +1,15 @@
 """Summarise tools/h16_vs_vendor.sh output: per implementation, the dominant
-kernel's average duration, effective clock, MFMA-busy fraction, LDS traffic,
-fabric bytes and L2 hit rate (per launch, counters summed over XCDs/SEs).
+kernel's average duration, effective clock, MFMA utilisation (from the
+calibrated MOPS counter, tools/pmc_metrics.py), fabric bytes and L2 hit rate
+(per launch, counters summed over XCDs/SEs).
 
-  python tools/pmc_compare.py <tag> <flops_per_launch>
+  python tools/pmc_compare.py <tag> <flops_per_launch> [dtype]
 """
 import csv, glob, json, os, sys
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_metrics  # noqa: E402
 tag, flops = sys.argv[1], float(sys.argv[2])
+dtype = sys.argv[3] if len(sys.argv) > 3 else "bf16"
 root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
 out = {}
 for impl in ("ours", "vendor"):
@@ -28,14 +32,6 @@ for impl in ("ours", "vendor"):
                 vals = [v[nm] for v in disp.values() if nm in v]
                 c[nm] = sum(vals) / len(vals)
     res = {"kernel": name[:120], "avg_ms": avg * 1e3, "tflops": flops / avg / 1e12, "counters": c}
-    if "GRBM_GUI_ACTIVE" in c:
-        cyc = c["GRBM_GUI_ACTIVE"] / 8.0
-        res["effective_clock_ghz"] = cyc / avg / 1e9
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-            res["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
-    if "FETCH_SIZE" in c:
-        res["fabric_read_GB"] = 2.0 * c["FETCH_SIZE"] * 1024 / 1e9
-    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
-        res["l2_hit"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    res.update(pmc_metrics.derive(c, avg, dtype, flops))
     out[impl] = res
 print(json.dumps(out, indent=1))

@@ -41,18 +41,19 @@ if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     res["note"] = "FETCH_SIZE x2 (gfx950 counts half of wide streaming reads) + WRITE_SIZE, KB -> bytes"
 if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
     res["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
-    # MFMA pipe-busy cycles summed over the 1024 SIMDs (64 per v_mfma_f64_16x16x4_f64,
-    # MI355X_MICROARCH.md: 32 per 32x32x16 bf16) over the GPU-busy cycles of one XCD
-    # (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
-    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
-    res["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cycles)
-    if stats:
-        rows = [r for r in csv.DictReader(open(stats[0])) if (r["Name"] == exact if exact else kpat in r["Name"])]
-        if rows:
-            secs = float(rows[0]["AverageNs"]) * 1e-9
-            res["effective_clock_ghz"] = cycles / secs / 1e9
-            res["kernel_avg_ms"] = secs * 1e3
+# MFMA utilisation from the calibrated MOPS counter (tools/pmc_metrics.py: the
+# SQ_VALU_MFMA_BUSY_CYCLES reading of rounds 1-3 was a pegged constant)
+dtype = key.split(":")[0]
+secs = None
+if stats and exact:
+    rows = [r for r in csv.DictReader(open(stats[0])) if r["Name"] == exact]
+    if rows:
+        secs = float(rows[0]["AverageNs"]) * 1e-9
+        res["kernel_avg_ms"] = secs * 1e3
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_metrics  # noqa: E402
+flops = float(sys.argv[4]) if len(sys.argv) > 4 else None
+res.update(pmc_metrics.derive(c, secs, dtype, flops))
 res["bench_key"] = key
 json.dump(res, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
 idx_path = os.path.join(prof, "traffic_index.json")
