@@ -43,7 +43,8 @@ template <int BM_, int WTM_ = 32, int SK_ = BK>
 struct Shape {
     static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW, SK = SK_;
     static constexpr int IMGA = BM * SK * 8, IMGB = BN * SK * 8, STAGE = IMGA + IMGB;
-    static constexpr int WAVES_PER_EU = NW * (BM_ == 128 && SK_ == 16 ? 2 : 1) / 4;  // waves resident per SIMD
+    // waves resident per SIMD: two workgroups per CU at SK = 16 (BM 64 / 128)
+    static constexpr int WAVES_PER_EU = NW * (BM_ <= 128 && SK_ == 16 ? 2 : 1) / 4;
 };
 
 // KC images: rows of SK doubles (128 B at SK 16, 256 B at SK 32); 16-B chunk c of
@@ -95,10 +96,16 @@ __device__ __forceinline__ void stage_img(const double* X, i64 ld, i64 rows, i64
             const int c = (l % CPR) ^ swz_kc<SK>(r);
             const i64 row = R + r < rows ? r : rows - 1 - R;  // rows past the edge: any valid data
             src.load(row * ld + 2 * c, img + ins * 1024);
-        } else {   // X(row, k) = X[row + k*ld]; k-rows of ROWS*8 B, 1 KiB per instruction
+        } else if constexpr (ROWS * 8 >= 1024) {  // X(row, k) = X[row + k*ld]; k-rows of ROWS*8 B
             constexpr int IPR = ROWS * 8 / 1024;  // instructions per k-row
             const int kk = ins / IPR;
             const int c = ((ins % IPR) * 64 + l) ^ ((kk & 1) << 3);
+            const i64 col = R + 2 * c <= rows - 2 ? 2 * c : rows - 2 - R;
+            src.load(col + kk * ld, img + ins * 1024);
+        } else {  // short k-rows (ROWS = 64: 512 B): several k-rows per 1-KiB instruction
+            constexpr int CPK = ROWS * 8 / 16, KPI = 1024 / (ROWS * 8);  // chunks per k-row, k-rows per instruction
+            const int kk = ins * KPI + l / CPK;
+            const int c = (l % CPK) ^ ((kk & 1) << 3);
             const i64 col = R + 2 * c <= rows - 2 ? 2 * c : rows - 2 - R;
             src.load(col + kk * ld, img + ins * 1024);
         }
@@ -295,6 +302,10 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // 16384^3; 32-deep slabs for one-workgroup-per-CU grids, 53.8 vs 60.6 TF at
     // 2048^3, profiles/r03_f64_small.log.)
     const i64 grid_wgs = (i64)((m + 127) / 128) * p.tiles_n * ((kmain + kchunk - 1) / kchunk);
+    // ELX_F64G_BM64 = W > 0: grids of at most W 128-row workgroups take 64-row
+    // tiles (four waves of 32 x 64, two workgroups per CU) instead
+    static const int bm64 = [] { const char* v = getenv("ELX_F64G_BM64"); return v ? atoi(v) : 0; }();
+    if (bm64 > 0 && grid_wgs <= bm64) return launch_shape<Shape<64, 32>>(ta, !tb, p, s);
     const int wtm = wtm_env ? wtm_env : ((!ta && tb) || grid_wgs <= 256) ? 32 : 64;
     if (wtm == 64) return launch_shape<Shape<128, 64>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);

@@ -86,6 +86,47 @@ def test_local_gemm_known_answer_exact(k):
     assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * A @ B - C)
 
 
+_SMALL_TILE_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from elemental_amd import _lib as L
+OPS = {"N": 0, "T": 1}
+bad = []
+for (m, n, k) in [(2048, 2048, 2072), (2000, 1990, 1056), (64, 128, 48), (190, 130, 4104)]:
+    for ta in "NT":
+        for tb in "NT":
+            rng = np.random.default_rng(k + m)
+            A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
+            B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(np.float64))
+            C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(np.float64))
+            dv = lambda X: torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+            dA, dB, dC = dv(A), dv(B), dv(C)
+            torch.cuda.synchronize()
+            L.call("elx_gemm_f64", OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0], dB.data_ptr(),
+                   B.shape[0], -1.0, dC.data_ptr(), m, None)
+            L.call("elx_device_synchronize")
+            got = dC.cpu().numpy().T
+            want = 2.0 * (A if ta == "N" else A.T) @ (B if tb == "N" else B.T) - C
+            if not np.array_equal(got, want):
+                bad.append((m, n, k, ta, tb))
+print("BAD", bad if bad else "none")
+"""
+
+
+def test_local_gemm_f64_64row_tiles_exact():
+    """The fp64 LDS-DMA kernel's 64-row tiles (ELX_F64G_BM64: RC images of
+    512-B k-rows, two per DMA instruction), every orientation, edges and the
+    k tail: exact on integer operands (run in a child, the knob is read once)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _SMALL_TILE_SCRIPT, root], capture_output=True, text=True,
+                       timeout=110, env=dict(os.environ, ELX_F64G_BM64="100000"))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    assert "BAD none" in p.stdout, p.stdout[-2000:]
+
+
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2048, 2072), (2000, 1990, 1056), (1024, 1024, 288)])
