@@ -47,6 +47,7 @@ struct FParams {
     // split-k (gridDim.y chunks): chunk z covers k in [z*kchunk, min(k, (z+1)*kchunk))
     // and writes C + z*zstride (the caller passes a workspace, alpha = 1, beta = 0)
     i64 kchunk, zstride;
+    int vec_c;  // C 16-B aligned with ldc % 4 == 0: the interior epilogue's 16-B accesses
 };
 
 __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
@@ -180,6 +181,27 @@ __global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParam
     // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
     const int g = l >> 4, c = l & 15;
     const i64 ib = m0 + wr * WTM + 4 * g, jb = n0 + wc * 64 + c;
+    if (p.vec_c && m0 + BM <= p.m && n0 + BN <= p.n) {
+        // interior tile: a 16-row block's C loads all issued before its first
+        // store (the guarded form below serializes load -> wait -> store per
+        // element, since the compiler cannot reorder loads across the stores)
+#pragma unroll
+        for (int mi = 0; mi < WS::MI; ++mi) {
+            f32x4 cv[4];
+            if (!BETA0) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    cv[ni] = *reinterpret_cast<const f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16);
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                f32x4 v = p.alpha * acc[mi][ni];
+                if (!BETA0) v += p.beta * cv[ni];
+                *reinterpret_cast<f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16) = v;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int mi = 0; mi < WS::MI; ++mi)
 #pragma unroll
@@ -244,7 +266,7 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
 hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
                             i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s) {
     FParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-              kchunk, m * n};
+              kchunk, m * n, (reinterpret_cast<uintptr_t>(C) & 15) == 0 && ldc % 4 == 0 && (kchunk >= kmain || m % 4 == 0)};
     const bool kca = ta, kcb = !tb;
     if (kca) return kcb ? launch_f<true, true>(p, s) : launch_f<true, false>(p, s);
     return kcb ? launch_f<false, true>(p, s) : launch_f<false, false>(p, s);
