@@ -26,6 +26,8 @@ LEFT, RIGHT = 0, 1  # El::LeftOrRight (types.hpp:418-422)
 NON_UNIT, UNIT = 0, 1  # El::UnitOrNonUnit (types.hpp:489-493)
 CPU, GPU = 0, 1
 F32, F64, F16, BF16 = 0, 1, 2, 3
+I32, I64, U8 = 4, 5, 6  # communication buffers only (elx_mpi_*, elx_comm_*)
+OP_SUM, OP_PROD, OP_MAX, OP_MIN = 0, 1, 2, 3
 (MAP_IDENTITY, MAP_NEGATE, MAP_ABS, MAP_SQUARE, MAP_SQRT, MAP_EXP, MAP_LOG, MAP_RELU, MAP_SIGMOID,
  MAP_RECIP, MAP_TANH) = range(11)
 (COMBINE_ADD, COMBINE_SUB, COMBINE_MUL, COMBINE_DIV, COMBINE_MAX, COMBINE_MIN, COMBINE_RELU_GRAD) = range(7)

@@ -539,7 +539,7 @@ ReduceOp ToOp(int op) {
 int elx_mpi_allgather(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
                       void* stream) {
     return Guard([&] {
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
         MpiRun(c, device, stream, send, b, recv, b * c->c->Size(), false,
                [&](const void* sb, void* rb, Device d, hipStream_t s) { c->c->AllGather(t, sb, rb, count, d, s); });
@@ -548,7 +548,7 @@ int elx_mpi_allgather(elx_comm_t c, int dtype, int device, const void* send, voi
 int elx_mpi_reduce_scatter(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv,
                            int64_t count, void* stream) {
     return Guard([&] {
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const ReduceOp o = ToOp(op);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
         MpiRun(c, device, stream, send, b * c->c->Size(), recv, b, false,
@@ -558,7 +558,7 @@ int elx_mpi_reduce_scatter(elx_comm_t c, int dtype, int device, int op, const vo
 int elx_mpi_allreduce(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv, int64_t count,
                       void* stream) {
     return Guard([&] {
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const ReduceOp o = ToOp(op);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
         MpiRun(c, device, stream, send, b, recv, b, false,
@@ -568,7 +568,7 @@ int elx_mpi_allreduce(elx_comm_t c, int dtype, int device, int op, const void* s
 int elx_mpi_alltoall(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
                      void* stream) {
     return Guard([&] {
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const int p = c->c->Size();
         const size_t b = static_cast<size_t>(count) * DTypeSize(t) * p;
         std::vector<Int> cnt(p, count), dsp(p);
@@ -581,7 +581,7 @@ int elx_mpi_alltoall(elx_comm_t c, int dtype, int device, const void* send, void
 int elx_mpi_bcast(elx_comm_t c, int dtype, int device, void* buf, int64_t count, int root, void* stream) {
     return Guard([&] {
         ELX_REQUIRE(root >= 0 && root < c->c->Size(), "bcast: root ", root, " outside the communicator");
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
         MpiRun(c, device, stream, buf, b, buf, b, true,
                [&](const void*, void* rb, Device d, hipStream_t s) { c->c->Bcast(t, rb, count, root, d, s); });
@@ -590,7 +590,7 @@ int elx_mpi_bcast(elx_comm_t c, int dtype, int device, void* buf, int64_t count,
 int elx_mpi_sendrecv(elx_comm_t c, int dtype, int device, const void* send, int64_t scount, int dest, void* recv,
                      int64_t rcount, int src, void* stream) {
     return Guard([&] {
-        const DType t = ToDType(dtype);
+        const DType t = ToCommDType(dtype);
         const size_t es = DTypeSize(t);
         MpiRun(c, device, stream, send, static_cast<size_t>(scount) * es, recv, static_cast<size_t>(rcount) * es,
                false, [&](const void* sb, void* rb, Device d, hipStream_t s) {

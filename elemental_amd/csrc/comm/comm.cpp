@@ -135,6 +135,9 @@ ncclDataType_t NcclType(DType t) {
     case DType::F64: return ncclFloat64;
     case DType::F16: return ncclFloat16;
     case DType::BF16: return ncclBfloat16;
+    case DType::I32: return ncclInt32;
+    case DType::I64: return ncclInt64;
+    case DType::U8: return ncclUint8;
     }
     throw LogicError("bad dtype");
 }
@@ -317,7 +320,7 @@ void Comm::ReduceScatter(DType t, const void* send, void* recv, Int count, Devic
         CheckNccl(ncclReduceScatter(send, recv, count, NcclType(t), NcclOp(op), nccl_, s), "ncclReduceScatter", nccl_);
         return;
     }
-    if (op != ReduceOp::SUM || t == DType::F16 || t == DType::BF16) {
+    if (op != ReduceOp::SUM || !(t == DType::F32 || t == DType::F64)) {
         HostFold(true, t, op, send, recv, count, dev, s);
         return;
     }
@@ -340,7 +343,7 @@ void Comm::AllReduce(DType t, const void* send, void* recv, Int count, Device de
         CheckNccl(ncclAllReduce(send, recv, count, NcclType(t), NcclOp(op), nccl_, s), "ncclAllReduce", nccl_);
         return;
     }
-    if (op != ReduceOp::SUM || t == DType::F16 || t == DType::BF16) {
+    if (op != ReduceOp::SUM || !(t == DType::F32 || t == DType::F64)) {
         HostFold(false, t, op, send, recv, count, dev, s);
         return;
     }
@@ -396,6 +399,12 @@ void Comm::HostFold(bool scatter, DType t, ReduceOp op, const void* send, void* 
         FoldRanks<double>(op, hr.data(), out.data(), count, size_);
     } else if (t == DType::F32) {
         FoldRanks<float>(op, hr.data(), out.data(), count, size_);
+    } else if (t == DType::I32) {
+        FoldRanks<int32_t>(op, hr.data(), out.data(), count, size_);
+    } else if (t == DType::I64) {
+        FoldRanks<int64_t>(op, hr.data(), out.data(), count, size_);
+    } else if (t == DType::U8) {
+        FoldRanks<uint8_t>(op, hr.data(), out.data(), count, size_);
     } else {
         const bool bf = t == DType::BF16;
         auto ld = [&](uint16_t v) { return bf ? BF16ToFloat(v) : HalfToFloat(v); };

@@ -66,7 +66,11 @@ int Guard(F&& f) {
     catch (...)                         { SetLastError("unknown exception"); return ELX_ERR_RUNTIME; }
 }
 
-enum class DType : int { F32 = ELX_F32, F64 = ELX_F64, F16 = ELX_F16, BF16 = ELX_BF16 };
+// F32..BF16: matrix element types; I32 / I64 / U8: communication buffers only
+// (ToCommDType), never a DistMatrix or kernel type (ToDType rejects them)
+enum class DType : int {
+    F32 = ELX_F32, F64 = ELX_F64, F16 = ELX_F16, BF16 = ELX_BF16, I32 = ELX_I32, I64 = ELX_I64, U8 = ELX_U8
+};
 
 inline size_t DTypeSize(DType t) {
     switch (t) {
@@ -74,11 +78,18 @@ inline size_t DTypeSize(DType t) {
     case DType::F64: return 8;
     case DType::F16: return 2;
     case DType::BF16: return 2;
+    case DType::I32: return 4;
+    case DType::I64: return 8;
+    case DType::U8: return 1;
     }
     throw LogicError("bad dtype");
 }
 inline DType ToDType(int t) {
     if (t < 0 || t > 3) throw LogicError(Cat("invalid dtype ", t));
+    return static_cast<DType>(t);
+}
+inline DType ToCommDType(int t) {
+    if (t < 0 || t > ELX_U8) throw LogicError(Cat("invalid dtype ", t, " for a collective"));
     return static_cast<DType>(t);
 }
 inline const char* DTypeName(DType t) {
@@ -87,6 +98,9 @@ inline const char* DTypeName(DType t) {
     case DType::F64: return "f64";
     case DType::F16: return "f16";
     case DType::BF16: return "bf16";
+    case DType::I32: return "i32";
+    case DType::I64: return "i64";
+    case DType::U8: return "u8";
     }
     return "?";
 }

@@ -40,6 +40,7 @@ template <> struct H<Brain16> {
     case DType::F32: { using S = float; __VA_ARGS__; break; }          \
     case DType::F16: { using S = Half16; __VA_ARGS__; break; }         \
     case DType::BF16: { using S = Brain16; __VA_ARGS__; break; }       \
+    default: throw LogicError(Cat("dtype ", DTypeName(t), " is not a matrix type")); \
     }
 
 template <typename S>
@@ -144,6 +145,7 @@ void cpu_convert(const Copy2D& d) {
     case DType::F32: { using T = float; __VA_ARGS__; break; }            \
     case DType::F16: { using T = kern::f16_t; __VA_ARGS__; break; }      \
     case DType::BF16: { using T = kern::bf16_t; __VA_ARGS__; break; }    \
+    default: throw LogicError(Cat("dtype ", DTypeName(t), " is not a matrix type")); \
     }
 }  // namespace
 
@@ -178,6 +180,8 @@ void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alp
                                   static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb,
                                   (float)beta, static_cast<uint16_t*>(C), ldc, s);
             break;
+        default:
+            throw LogicError(Cat("dtype ", DTypeName(t), " is not a matrix type"));
         }
         check(e, "gemm_mfma");
         return;

@@ -89,6 +89,8 @@ void MakeUniform(DistMatrix& A, double center, double radius) {
                 for (Int i = 0; i < m; ++i) h[i + j * m] = FloatToBF16(uni(gen));
             break;
         }
+        default:
+            throw LogicError(Cat("MakeUniform: dtype ", DTypeName(A.Type()), " is not a matrix type"));
         }
         A.SetLocal(host.data(), m);
     }

@@ -15,8 +15,9 @@ import torch.distributed as dist
 
 from . import _lib as L
 
-_NP = {L.F32: np.float32, L.F64: np.float64, L.F16: np.float16, L.BF16: np.int16}
-_ES = {L.F32: 4, L.F64: 8, L.F16: 2, L.BF16: 2}
+_NP = {L.F32: np.float32, L.F64: np.float64, L.F16: np.float16, L.BF16: np.int16, L.I32: np.int32,
+       L.I64: np.int64, L.U8: np.uint8}
+_ES = {L.F32: 4, L.F64: 8, L.F16: 2, L.BF16: 2, L.I32: 4, L.I64: 8, L.U8: 1}
 
 
 def _arr(ptr: int, count: int, dtype: int) -> torch.Tensor:

@@ -253,6 +253,10 @@ template <> struct TypeCode<float> { static constexpr int value = ELX_F32; };
 template <> struct TypeCode<double> { static constexpr int value = ELX_F64; };
 template <> struct TypeCode<gpu_half_type> { static constexpr int value = ELX_F16; };
 template <> struct TypeCode<bfloat16> { static constexpr int value = ELX_BF16; };
+// communication-only element types (El::mpi on Int / int / byte buffers)
+template <> struct TypeCode<std::int32_t> { static constexpr int value = ELX_I32; };
+template <> struct TypeCode<std::int64_t> { static constexpr int value = ELX_I64; };
+template <> struct TypeCode<unsigned char> { static constexpr int value = ELX_U8; };
 template <typename T> double ToDouble(T x) { return static_cast<double>(x); }
 template <typename T> T FromDouble(double v) { return static_cast<T>(v); }
 // 16-bit values cross the boundary as their exact double widening

@@ -72,6 +72,12 @@ extern "C" {
 #define ELX_F64  1
 #define ELX_F16  2   /* gpu_half_type (rocblas_half), include/hydrogen/utils/HalfPrecision.hpp:123 */
 #define ELX_BF16 3   /* new: no reference counterpart */
+/* element types of the communication entry points only (elx_mpi_*, elx_comm_*):
+ * El::mpi's collectives also move Int / int / byte buffers (El::Int is 64-bit
+ * in an EL_USE_64BIT_INTS build, 32-bit by default) */
+#define ELX_I32  4
+#define ELX_I64  5
+#define ELX_U8   6
 /* entrywise functors for elx_entrywise_map (the C-ABI cannot carry a device
  * lambda; include/El.hpp maps them to El::EntrywiseFn)      */
 #define ELX_MAP_IDENTITY 0

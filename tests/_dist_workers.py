@@ -839,7 +839,7 @@ def mpi_typed_worker(rank: int, world: int, port: int, device: int):
         def get(b):
             return b
     fmts = ((el.F64, "f64", np.float64), (el.F32, "f32", np.float32), (el.F16, "f16", np.float16),
-            (el.BF16, "bf16", np.uint16))
+            (el.BF16, "bf16", np.uint16), (L.I32, "i32", np.int32), (L.I64, "i64", np.int64))
     folds = {0: lambda a, b: b + a, 1: lambda a, b: b * a, 2: np.maximum, 3: np.minimum}
 
     def enc(x, fmt, npdt):  # exact small integers in the storage format
@@ -848,7 +848,7 @@ def mpi_typed_worker(rank: int, world: int, port: int, device: int):
         return np.asarray(x, dtype=npdt)
 
     def dec(x, fmt):
-        return oracle.to_f64(x, fmt)
+        return np.asarray(x).astype(np.float64) if fmt in ("i32", "i64") else oracle.to_f64(x, fmt)
 
     try:
         def check(c, tag):
@@ -905,6 +905,13 @@ def mpi_typed_worker(rank: int, world: int, port: int, device: int):
                 L.call("elx_mpi_sendrecv", c.h, dt, device, ptr(send), sc_, (r + 1) % p, ptr(recv), rc_,
                        (r - 1) % p, None)
                 assert np.array_equal(dec(get(recv), fmt)[:rc_], vals((r - 1) % p, 4)[:rc_]), (tag, fmt, "sendrecv")
+            # bytes (El::byte buffers): gather and broadcast, bit-exact
+            if p > 0:
+                mine = buf(np.arange(5, dtype=np.uint8) + 17 * r)
+                out = buf(np.zeros(5 * p, dtype=np.uint8))
+                L.call("elx_mpi_allgather", c.h, L.U8, device, ptr(mine), ptr(out), 5, None)
+                want = np.concatenate([np.arange(5, dtype=np.uint8) + 17 * q for q in range(p)])
+                assert np.array_equal(np.asarray(get(out)).astype(np.uint8), want), (tag, "u8")
             # error mapping: a bad op and a bad root are LogicErrors
             x = buf(np.zeros(2))
             for call in (lambda: L.call("elx_mpi_allreduce", c.h, el.F64, device, 9, ptr(x), ptr(x), 2, None),

@@ -388,6 +388,18 @@ int main() {
         try { El::mpi::Broadcast(B.Buffer(), n, p, comm, si); }
         catch (const El::LogicError&) { threw_c = true; }
         EXPECT(threw_c);
+        // Int / int / byte buffers (host memory, any device tag)
+        {
+            const El::Int xi = me + 1;
+            EXPECT(El::mpi::AllReduce(xi, El::mpi::SUM, comm, El::SyncInfo<El::Device::CPU>{}) ==
+                   (El::Int)p * (p + 1) / 2);
+            std::int32_t v32[3] = {me, -me, 7};
+            El::mpi::AllReduce(v32, 3, El::mpi::MAX, comm, El::SyncInfo<El::Device::CPU>{});
+            EXPECT(v32[0] == p - 1 && v32[1] == 0 && v32[2] == 7);
+            std::vector<unsigned char> bytes(4 * p), mine = {1, 2, 3, (unsigned char)me};
+            El::mpi::AllGather(mine.data(), 4, bytes.data(), 4, comm, El::SyncInfo<El::Device::CPU>{});
+            EXPECT(bytes[4 * (p - 1) + 3] == (unsigned char)(p - 1) && bytes[1] == 2);
+        }
         // a split-off self communicator works the same way
         const El::mpi::Comm self = El::mpi::COMM_SELF();
         El::mpi::AllReduce(S.LockedBuffer(), T.Buffer(), n, El::mpi::SUM, self, si);
