@@ -9,7 +9,7 @@ ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-c3-1gpu $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG} -o bench -- python3 $R/bench.py $ARGS > $R/gpurun_out/prof_${TAG}_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; case $rc in 124|137|134|139) exit $rc;; esac
 i=0
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE"; do
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d $R/gpurun_out/prof_${TAG}_pmc$i -o pmc -- python3 $R/bench.py $ARGS > $R/gpurun_out/prof_${TAG}_pmc$i.log 2>&1
   rc=$?; echo "pmc $i ($pmc) rc=$rc"; case $rc in 124|137|134|139) exit $rc;; esac

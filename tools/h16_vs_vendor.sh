@@ -11,8 +11,8 @@ for impl in ${IMPLS:-ours vendor}; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_${impl}_trace -o t -- python3 $R/tools/prof_gemm.py "$@" 10 $V > $R/gpurun_out/${TAG}_${impl}_trace.log 2>&1
   rc=$?; echo "$impl trace rc=$rc"; case $rc in 124|137|134|139) exit $rc;; esac
   i=0
-  # MFMA utilisation from the MOPS counters (tools/pmc_metrics.py); the pegged
-  # SQ_VALU_MFMA_BUSY_CYCLES stays in pass 4 as a record of its reading
+  # MFMA utilisation from the MOPS counters, cross-checked by the busy cycles
+  # (both calibrated: tools/pmc_metrics.py, profiles/r04_mfma_calib.log)
   for pmc in "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS" \
              "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VMEM SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES"; do
     i=$((i+1))

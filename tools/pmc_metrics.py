@@ -1,34 +1,33 @@
 """Derived PMC metrics shared by tools/summarize_profiles.py and tools/pmc_compare.py.
 
-Round 4 repair of the "MFMA busy" figure: rounds 1-3 divided
-SQ_VALU_MFMA_BUSY_CYCLES by GRBM_GUI_ACTIVE, but that counter read an exact
-power of two in every profile (2^41 for every fp64 launch, 2^36 for every C5
-launch, 2^33 for two different kernels), so the quotient only scaled the
-inverse kernel time.  The MFMA utilisation is now derived from the MOPS
-counters, which tools/mfma_calib.hip / tools/pmc_calib.sh calibrate against
-kernels of known MFMA count (SQ_INSTS_VALU_MFMA_MOPS_* = FLOPs / 512):
+Round 4 calibration of the MFMA counters (tools/mfma_calib.hip under
+tools/pmc_calib.sh, profiles/r04_mfma_calib.log: kernels of known MFMA count):
+  SQ_INSTS_VALU_MFMA_MOPS_{F64,BF16}  = FLOPs / 512 exactly (4 per f64 16x16x4,
+                                        32 per bf16 16x16x32);
+  SQ_VALU_MFMA_BUSY_CYCLES            = sum over MFMAs of their pipe cycles
+                                        exactly (64 per f64 16x16x4, 16 per
+                                        bf16 16x16x32), linear in the count.
+The round-3 verdict read the power-of-two values of the busy counter in every
+GEMM profile (2^41 at C2, 2^36 at C5, 2^33 at bf16 16384^3) as a stuck
+counter; they are the exact MFMA cycle counts of power-of-two problems
+(32768^3 / 2048 FLOP x 64 cycles = 2^41).  Both counters therefore give the
+same utilisation, reported twice as a cross-check:
 
-  mfma_util = MOPS * 512 / (FLOP per cycle per CU * 256 CUs * cycles)
+  mfma_util      = MOPS * 512 / (FLOP per cycle per CU * 256 CUs * cycles)
+  mfma_util_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * cycles)
 
-with cycles = GRBM_GUI_ACTIVE / 8 (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
-and FLOP per cycle per CU = dense peak / (256 CUs x 2.4 GHz): f64 128, f32 256,
-bf16 / f16 4096 (v_mfma_f64_16x16x4_f64 = 2048 FLOP in 64 cycles per SIMD,
-v_mfma_f32_16x16x32_bf16 = 16384 FLOP in 16, MI355X_MICROARCH.md).  That is
-the fraction of the MFMA pipes' cycles spent on useful MFMAs at the clock the
-kernel actually ran at; `effective_clock_ghz` carries the clock part of the
-gap to the 2.4 GHz peak.
+with cycles = GRBM_GUI_ACTIVE / 8 (GRBM_GUI_ACTIVE is summed over the 8 XCDs;
+the calibration's f64 probe: 52.4 M / 8 = 6.55 M cycles in 3.33 ms = 1.97 GHz,
+busy 0.625 = its 40.3 TF over the 64.5 TF peak at that clock) and FLOP per
+cycle per CU = dense peak / (256 CUs x 2.4 GHz): f64 128, f32 256, bf16 / f16
+4096.  That is the fraction of the MFMA pipes' cycles spent on MFMAs at the
+clock the kernel actually ran at; `effective_clock_ghz` carries the clock part
+of the gap to the 2.4 GHz peak.
 """
 FLOP_PER_CYCLE_CU = {"f64": 128.0, "f32": 256.0, "bf16": 4096.0, "f16": 4096.0}
 MOPS_COUNTER = {"f64": "SQ_INSTS_VALU_MFMA_MOPS_F64", "f32": "SQ_INSTS_VALU_MFMA_MOPS_F32",
                 "bf16": "SQ_INSTS_VALU_MFMA_MOPS_BF16", "f16": "SQ_INSTS_VALU_MFMA_MOPS_F16"}
 NCU = 256
-
-
-def pegged(v: float) -> bool:
-    """An exact power of two of at least 2^30: the saturated / stuck reading
-    rounds 1-3 took for MFMA busy cycles."""
-    iv = int(v)
-    return v == iv and iv >= (1 << 30) and (iv & (iv - 1)) == 0
 
 
 def derive(c: dict, avg_s: float | None, dtype: str, flops: float | None = None) -> dict:
@@ -46,8 +45,9 @@ def derive(c: dict, avg_s: float | None, dtype: str, flops: float | None = None)
             out["mfma_util"] = mops * 512.0 / (FLOP_PER_CYCLE_CU[dtype] * NCU * cyc)
     busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
     if busy is not None:
-        out["mfma_busy_cycles_raw"] = busy
-        out["mfma_busy_cycles_pegged"] = pegged(busy)
+        out["mfma_busy_cycles"] = busy
+        if cyc > 0:
+            out["mfma_util_busy"] = busy / (4.0 * NCU * cyc)
     if "FETCH_SIZE" in c:
         out["fabric_read_bytes"] = 2.0 * c["FETCH_SIZE"] * 1024.0  # gfx950: FETCH_SIZE counts half of wide reads
     if "WRITE_SIZE" in c:
