@@ -67,11 +67,26 @@ def stage(name: str, seconds: float):
 def cpu_baseline(seconds_target: float = 10.0) -> dict:
     """The CPU leg (BASELINE.md §3): C1 (BASELINE.json configs[0]), El::Gemm NN
     fp64 4096^3 on a 2x2 grid, run as the reference's CPU path runs it: SUMMA_NNC
-    over 4 processes with nb = 128 all-gathers (gloo) and a blocked OpenMP dgemm
-    for the local updates (oracle/cpu_summa.py over oracle/cpu_gemm.c, the port
-    of the reference's BLAS call), on the box's cores, for ~seconds_target."""
+    over 4 processes with nb = 128 all-gathers and one MKL dgemm_ per panel
+    (oracle/cpu_summa.c), for ~seconds_target.  On 8 cores (2 per rank, each
+    rank pinned to its own): the core count of the reference's own C1 figure
+    (0.477 TF on 8 cores), so the two compare per core; the
+    same run on every core the box grants (16) is reported beside it.
+    Placement measured on the box (profiles/r04_cpu_baseline_sweep.log):
+    1 / 2 / 4 MKL threads per rank = 69 / 63 / 53 GF per core."""
+    import oracle
     from oracle import cpu_summa
-    return cpu_summa.run(n=4096, nb=128, r=2, c=2, seconds=seconds_target)
+    out = cpu_summa.run(n=4096, nb=128, r=2, c=2, seconds=seconds_target, cores=8)
+    allc = oracle.cpu_threads()
+    if allc > 8:
+        try:
+            wide = cpu_summa.run(n=4096, nb=128, r=2, c=2, seconds=seconds_target / 2, cores=allc)
+            out["all_cores"] = {"value": wide["value"], "cores": wide["cores"]}
+        except Exception as e:  # context only
+            out["all_cores"] = {"error": str(e)}
+    out["per_core_gflops"] = round(out["value"] * 1e3 / out["cores"], 1)
+    out["reference_per_core_gflops"] = round(477.0 / 8, 1)
+    return out
 
 
 def measured_traffic(dtype: str, n: int, world: int):
