@@ -111,6 +111,20 @@ __device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l)
     }
 }
 
+// s_waitcnt through the builtin, not inline asm: hipcc's waitcnt pass sees a
+// builtin wait and drops the conservative waits it would otherwise add for
+// fragment registers whose LDS reads an opaque asm wait already retired (at
+// bf16 TN the asm form left 72 spurious "s_waitcnt lgkmcnt(7)" among the MFMAs
+// of every five K-tiles; removing them: +0.5-2.4 %, bf16 NN 32768^3 1394-1413 ->
+// 1428 TF in one process, profiles/r04_h16_waitcnt_ab.log).  gfx9 encoding: vmcnt [3:0] and [15:14], expcnt
+// [6:4], lgkmcnt [11:8]; the fields not waited on are at their maxima.
+template <int VM, int LGKM>
+__device__ __forceinline__ void wait_cnt() {
+    static_assert(VM >= 0 && VM <= 63 && LGKM >= 0 && LGKM <= 15, "waitcnt field range");
+    __builtin_amdgcn_s_waitcnt((VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (LGKM << 8));
+}
+constexpr int NOWAIT_VM = 63, NOWAIT_LGKM = 15;
+
 __device__ __forceinline__ void bar8() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
@@ -378,7 +392,7 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         for (int u = 0; u < 8; ++u)
             piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
     }
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    wait_cnt<16, NOWAIT_LGKM>();
     bar8();
     Sets X, Y;
 #pragma unroll
@@ -386,7 +400,7 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         X.a[q] = frag<KCA>(lds + wr * HALF, q * 16, 0, l);
         X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_cnt<NOWAIT_VM, 0>();
     // One K-tile; J = t % 5 makes every slot a compile-time offset of the LDS
     // base (the loop is unrolled by the ring length), so the fragment reads and
     // the DMA destinations need no address arithmetic in the loop.
@@ -397,13 +411,12 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         // (t,0): stage A_{t+2} into B_{t-1}'s slot
         w4::kstep<BF16, KCA, KCB, BUF, false>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
                                                  lds + st0 * UNIT, kt(t + 2), acc, X, Y);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_cnt<8, 0>();
         bar8();
         // (t,1): stage B_{t+2} into A_t's slot
         w4::kstep<BF16, KCA, KCB, BUF, true>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
                                                 lds + st1 * UNIT, kt(t + 2), acc, Y, X);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_cnt<NOWAIT_VM, 0>();
     };
     for (int t = 0; t < nt; t += NSLOT) {
         ktile(std::integral_constant<int, 0>{}, t);
@@ -417,140 +430,10 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
-// ---------------------------------------------------------------------------
-// Two-barrier schedule (round 4; ELX_H16_SCHED=2 while it is A/B-measured):
-// the same tile, waves, fragments and DMA pieces as gemm_h4w_kernel, but every
-// wave's fragment reads and every wave's DMA issue sit in different barrier
-// intervals, as hipBLASLt's MT256x256x64 bf16 loop does (its disassembly: 32
-// ds_read_b128 in ~47 MFMAs after one barrier, 16 DMA pieces in ~81 MFMAs
-// after the other).  A piece issued while any wave of the CU is reading
-// fragments costs 100-185 cycles instead of ~60 (MI355X_MICROARCH.md, LDS-DMA
-// piece row); the one-barrier loop lets them overlap across waves.
-// Per K-tile t (two k-steps, fragment sets X = (t,0), Y = (t,1)):
-//   R1: MFMAs 0-15 of (t,0) on X; read Y from K-tile t.    lgkmcnt(0), barrier B1
-//   D1: MFMAs 16-63 of (t,0) on X; stage A_{t+2} into K-tile t's A unit (8 pieces)
-//   D2: MFMAs 0-47 of (t,1) on Y; stage B_{t+2} into K-tile t's B unit (8 pieces)
-//                                                        vmcnt(16), barrier B2
-//   R2: MFMAs 48-63 of (t,1) on Y; read X' = (t+1,0) from K-tile t+1.
-// LDS: two K-tile buffers (K-tile t in buffer t & 1: A unit, B unit), 128 KiB.
-// WAR: K-tile t's units are read for the last time in R1 (and in the previous
-// R2), retired by the lgkmcnt(0) every wave passes before B1; they are
-// restaged (with K-tile t+2) only after B1.  RAW: R1 and R2 read K-tiles t and
-// t+1 after B2 of the previous / this K-tile, before which every wave's
-// vmcnt(16) retired all but its 16 newest pieces (K-tile t+2's): K-tile t+1
-// has landed.  Tail: pieces of K-tiles past the end re-stage the last K-tile
-// into a buffer nobody reads again (the counted waits stay exact).
-// ---------------------------------------------------------------------------
-namespace w2 {
-using namespace w4;
-// MFMAs I0..I1-1 of a k-step on `cur` (MFMA i: accumulator (i>>3, i&7)).
-// RD: the first 16 also issue the 16 fragment reads of `nxt` from (rdA, rdB),
-// k-step srd, in the order the next k-step consumes them (a0, b0..b7, a1..a7).
-// DM: every DS-th issues one of this wave's 8 pieces of operand SB ? B : A at k0 into `st`.
-template <bool BF16, bool KCA, bool KCB, bool BUF, int I0, int I1, bool RD, bool DM, bool SB, int DS>
-__device__ __forceinline__ void seg(const H2Params& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
-                                    const Pieces& pc, const lds_char* __restrict__ rdA,
-                                    const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
-                                    f32x4 (&acc)[8][8], const Sets& cur, Sets& nxt) {
-#pragma unroll
-    for (int i = I0; i < I1; ++i) {
-        mfma_acc<BF16>(acc[i >> 3][i & 7], cur.a[i >> 3], cur.b[i & 7]);
-        if constexpr (DM) {
-            if ((i - I0) % DS == 0 && (i - I0) / DS < 8) {
-                const int u = (i - I0) / DS;
-                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
-            }
-        }
-        if constexpr (RD) {
-            const int f = i - I0;
-            if (f == 0) nxt.a[0] = frag<KCA>(rdA + wr * HALF, 0, srd, l);
-            else if (f <= 8) nxt.b[f - 1] = frag<KCB>(rdB + wc * HALF, (f - 1) * 16, srd, l);
-            else if (f < 16) nxt.a[f - 8] = frag<KCA>(rdA + wr * HALF, (f - 8) * 16, srd, l);
-        }
-    }
-}
-}  // namespace w2
-
-template <bool BF16, bool KCA, bool KCB, bool BUF>
-__global__ __launch_bounds__(256, 1) void gemm_h2b_kernel(H2Params p) {
-    using namespace w4;
-    __shared__ __attribute__((aligned(1024))) char lds_raw[4 * UNIT];
-    lds_char* lds = (lds_char*)lds_raw;
-
-    const int tid = threadIdx.x, l = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;
-    int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
-    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
-
-    Pieces pc;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
-        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
-        pc.offA[u] = (int)(pc.gA[u] * 2);
-        pc.offB[u] = (int)(pc.gB[u] * 2);
-    }
-
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
-
-    const int nt = (int)(p.k / BK);
-    auto kt = [&](int t) { return (i64)min(t, nt - 1) * BK; };
-    // prologue: K-tile 0 into buffer 0, K-tile 1 into buffer 1; K-tile 0 landed; X = (0,0)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
-    }
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    bar8();
-    Sets X, Y;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        X.a[q] = frag<KCA>(lds + wr * HALF, q * 16, 0, l);
-        X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    auto ktile = [&](auto jc, int t) {
-        constexpr int J = decltype(jc)::value;  // t & 1: compile-time buffer offsets
-        lds_char* const curA = lds + (2 * J) * UNIT;
-        lds_char* const curB = lds + (2 * J + 1) * UNIT;
-        const lds_char* const nxtA = lds + (2 * (J ^ 1)) * UNIT;
-        const lds_char* const nxtB = lds + (2 * (J ^ 1) + 1) * UNIT;
-        w2::seg<BF16, KCA, KCB, BUF, 0, 16, true, false, false, 1>(p, m0, n0, w, l, wr, wc, pc, curA, curB, 1, nullptr,
-                                                                   0, acc, X, Y);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        bar8();  // B1
-        w2::seg<BF16, KCA, KCB, BUF, 16, 64, false, true, false, 6>(p, m0, n0, w, l, wr, wc, pc, nullptr, nullptr, 0,
-                                                                    curA, kt(t + 2), acc, X, Y);
-        w2::seg<BF16, KCA, KCB, BUF, 0, 48, false, true, true, 6>(p, m0, n0, w, l, wr, wc, pc, nullptr, nullptr, 0,
-                                                                  curB, kt(t + 2), acc, Y, X);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        bar8();  // B2
-        w2::seg<BF16, KCA, KCB, BUF, 48, 64, true, false, false, 1>(p, m0, n0, w, l, wr, wc, pc, nxtA, nxtB, 0,
-                                                                    nullptr, 0, acc, Y, X);
-    };
-    // unrolled by four K-tiles: at two, the register allocator spilled fragment
-    // sets across the back edge (260 VGPRs at bf16 NN); at four it does not
-    for (int t = 0; t < nt; t += 4) {
-        ktile(std::integral_constant<int, 0>{}, t);
-        if (t + 1 < nt) ktile(std::integral_constant<int, 1>{}, t + 1);
-        if (t + 2 < nt) ktile(std::integral_constant<int, 0>{}, t + 2);
-        if (t + 3 < nt) ktile(std::integral_constant<int, 1>{}, t + 3);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
-    w4::settle(acc);
-    w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
-}
+// (Measured and removed in round 4: a two-barrier loop that keeps every wave's
+// fragment reads and every wave's DMA issue in different barrier intervals, as
+// hipBLASLt's MT256x256x64 loop does — correct, but 1-6 % slower than this
+// one-barrier loop on every orientation, profiles/r04_h16_two_barrier_ab.log.)
 
 template <bool BF16, bool KCA, bool KCB>
 hipError_t launch_h16(const H2Params& p, hipStream_t s) {
@@ -558,12 +441,6 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
     // global (64-bit address) form
     const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
     const dim3 grid(p.tiles_m * p.tiles_n);
-    const char* sv = getenv("ELX_H16_SCHED");  // per call: A/B tools interleave values
-    if (sv && sv[0] == '2') {
-        if (buf) hipLaunchKernelGGL((gemm_h2b_kernel<BF16, KCA, KCB, true>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((gemm_h2b_kernel<BF16, KCA, KCB, false>), grid, dim3(256), 0, s, p);
-        return hipGetLastError();
-    }
     if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false>), grid, dim3(256), 0, s, p);
     return hipGetLastError();
