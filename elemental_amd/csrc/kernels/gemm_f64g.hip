@@ -33,18 +33,22 @@ namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BN = 128, BK = 16, GROUP_M = 8;
+constexpr int BK = 16, GROUP_M = 8;
 // Tile shape: BM = 128 rows, slab depth SK = 16 (two 32-KiB stages: two
 // workgroups per CU); wave tiles WTM x 64 with WTM = 32 (2 x 4 accumulators,
 // 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read per MFMA, half
 // the waves).  (The template also admits BM = 256 and SK = 32, both measured
 // slower and no longer launched.)
-template <int BM_, int WTM_ = 32, int SK_ = BK>
+// BN_ x WTN_: the N side likewise (128 x 64 everywhere but the 64 x 64 tiles
+// of grids with few 128 x 128 tiles).
+template <int BM_, int WTM_ = 32, int SK_ = BK, int BN_ = 128, int WTN_ = 64>
 struct Shape {
-    static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, NW = 2 * WM, NT = 64 * NW, SK = SK_;
+    static constexpr int BM = BM_, WTM = WTM_, MI = WTM_ / 16, WM = BM_ / WTM_, SK = SK_;
+    static constexpr int BN = BN_, WTN = WTN_, NI = WTN_ / 16, WN = BN_ / WTN_, NW = WM * WN, NT = 64 * NW;
     static constexpr int IMGA = BM * SK * 8, IMGB = BN * SK * 8, STAGE = IMGA + IMGB;
-    // waves resident per SIMD: two workgroups per CU at SK = 16 (BM 64 / 128)
-    static constexpr int WAVES_PER_EU = NW * (BM_ <= 128 && SK_ == 16 ? 2 : 1) / 4;
+    // waves resident per SIMD: two workgroups per CU at SK = 16 (BM 64 / 128), and
+    // four of the 32-KiB 64 x 64 tiles
+    static constexpr int WAVES_PER_EU = BM_ == 64 && BN_ == 64 ? 4 : NW * (BM_ <= 128 && SK_ == 16 ? 2 : 1) / 4;
 };
 
 // KC images: rows of SK doubles (128 B at SK 16, 256 B at SK 32); 16-B chunk c of
@@ -133,24 +137,24 @@ struct Frame {
 // waitcnt pass does not drain the in-flight DMA before the ds_reads.
 template <typename SH, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
-                                     const lds_char* __restrict__ cur, f64x4 (&acc)[SH::MI][4]) {
+                                     const lds_char* __restrict__ cur, f64x4 (&acc)[SH::MI][SH::NI]) {
     if (more) {
         stage_img<BUF, KCA, SH::BM, SH::NW, SH::SK>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<BUF, KCB, BN, SH::NW, SH::SK>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
+        stage_img<BUF, KCB, SH::BN, SH::NW, SH::SK>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
     }
     const lds_char* Ai = cur;
     const lds_char* Bi = cur + SH::IMGA;
 #pragma unroll
     for (int s = 0; s < SH::SK / 4; ++s) {
-        double a[SH::MI], b[4];
+        double a[SH::MI], b[SH::NI];
 #pragma unroll
         for (int mi = 0; mi < SH::MI; ++mi) a[mi] = opnd<KCA, SH::BM, SH::SK>(Ai, f.wr * SH::WTM + mi * 16, s, f.l);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = opnd<KCB, BN, SH::SK>(Bi, f.wc * 64 + ni * 16, s, f.l);
+        for (int ni = 0; ni < SH::NI; ++ni) b[ni] = opnd<KCB, SH::BN, SH::SK>(Bi, f.wc * SH::WTN + ni * 16, s, f.l);
 #pragma unroll
         for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < SH::NI; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
     }
 }
@@ -160,12 +164,12 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
 // (profiles/r01_f64_buf.log).
 template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF>
 __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GParams p) {
-    constexpr int BM = SH::BM, STAGE = SH::STAGE;
+    constexpr int BM = SH::BM, BN = SH::BN, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;  // WM (M) x 2 (N) waves of WTM x 64
+    const int wr = w / SH::WN, wc = w % SH::WN;  // WM (M) x WN (N) waves of WTM x WTN
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
@@ -178,11 +182,11 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
     }
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
-    f64x4 acc[SH::MI][4];
+    f64x4 acc[SH::MI][SH::NI];
 #pragma unroll
     for (int a = 0; a < SH::MI; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
+        for (int b = 0; b < SH::NI; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / SH::SK);
     stage_img<BUF, KCA, BM, SH::NW, SH::SK>(p.A, p.lda, p.m, m0, 0, lds, w, l);
@@ -199,21 +203,21 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
 
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
     const int g = l >> 4, c = l & 15;
-    const i64 ib = m0 + wr * SH::WTM, jb = n0 + wc * 64;
+    const i64 ib = m0 + wr * SH::WTM, jb = n0 + wc * SH::WTN;
     if (m0 + BM <= p.m && n0 + BN <= p.n) {
         // interior tile: every C load issued before the first store (the guarded
         // form below serializes load -> wait -> store per element)
 #pragma unroll
         for (int mi = 0; mi < SH::MI; ++mi) {  // 16 loads in flight per 16-row block (VGPR budget: 4 waves per SIMD)
-            double cv[4][4];
+            double cv[SH::NI][4];
             if (!BETA0) {
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < SH::NI; ++ni)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r];
             }
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < SH::NI; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const double v = p.alpha * acc[mi][ni][r];
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
 #pragma unroll
     for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
+        for (int ni = 0; ni < SH::NI; ++ni) {
             const i64 j = jb + ni * 16 + c;
             if (j >= p.n) continue;
             double* col = p.C + j * p.ldc;
@@ -256,9 +260,10 @@ hipError_t launch_b(const GParams& p, dim3 grid, hipStream_t s) {
 template <typename SH, bool KCA, bool KCB>
 hipError_t launch_g(GParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
+    p.tiles_n = (int)((p.n + SH::BN - 1) / SH::BN);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
     static const bool global_only = [] { const char* v = getenv("ELX_F64G_STAGE"); return v && v[0] == 'g'; }();
-    if (!global_only && dma_fits(KCA ? SH::BM : SH::SK, p.lda, 8) && dma_fits(KCB ? BN : SH::SK, p.ldb, 8))
+    if (!global_only && dma_fits(KCA ? SH::BM : SH::SK, p.lda, 8) && dma_fits(KCB ? SH::BN : SH::SK, p.ldb, 8))
         return launch_b<SH, KCA, KCB, true>(p, grid, s);
     return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
@@ -271,6 +276,20 @@ hipError_t launch_shape(bool kca, bool kcb, const GParams& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
+// 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU) for grids with
+// fewer than two 128 x 128 tiles per CU but at least two 64 x 64 ones, whole k
+// (no split-k partials); ELX_F64G_T64 = 0 never, 2 always (tests).
+int t64_mode() {
+    static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
+    return v;
+}
+bool t64_tiles(i64 m, i64 n) {
+    const int mode = t64_mode();
+    if (mode != 1) return mode == 2;
+    const i64 t128 = (m + 127) / 128 * ((n + 127) / 128), t64 = (m + 63) / 64 * ((n + 63) / 64);
+    return t128 < 512 && t64 >= 512;
+}
+
 }  // namespace
 
 DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const double* A, i64 lda, const double* B,
@@ -278,7 +297,8 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
                     (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
-    return dma_plan(ok, (m + 127) / 128 * ((n + BN - 1) / BN), k, BK);
+    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
+    return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 
 // C = alpha op(A)(:, :kmain) op(B)(:kmain, :) + beta C (kmain a multiple of 16, split
@@ -291,7 +311,8 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
         return g >= 1 ? g : 1;
     }();
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
-    GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, (int)((n + BN - 1) / BN), kchunk, m * n, gm, rm};
+    GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0, kchunk, m * n, gm, rm};
+    if (t64_tiles(m, n)) return launch_shape<Shape<64, 32, BK, 64, 32>>(ta, !tb, p, s);
     // wave tile: 64 x 64 (four waves) measured +1.5-2 % for NN/TN/TT; NT (both
     // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();
@@ -300,12 +321,10 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // (4096^3 and up: the four-wave split stays ahead; profiles/r03_f64_small.log).
     // (Measured and removed in round 4: 256-row tiles, 68.6-72.6 vs 74.1 TF at
     // 16384^3; 32-deep slabs for one-workgroup-per-CU grids, 53.8 vs 60.6 TF at
-    // 2048^3, profiles/r03_f64_small.log.)
-    const i64 grid_wgs = (i64)((m + 127) / 128) * p.tiles_n * ((kmain + kchunk - 1) / kchunk);
-    // ELX_F64G_BM64 = W > 0: grids of at most W 128-row workgroups take 64-row
-    // tiles (four waves of 32 x 64, two workgroups per CU) instead
-    static const int bm64 = [] { const char* v = getenv("ELX_F64G_BM64"); return v ? atoi(v) : 0; }();
-    if (bm64 > 0 && grid_wgs <= bm64) return launch_shape<Shape<64, 32>>(ta, !tb, p, s);
+    // 2048^3, profiles/r03_f64_small.log; 64 x 128 tiles, no gain,
+    // profiles/r04_small_shapes_ab.log; an LDS ring of 3 / 4 slabs for one
+    // workgroup per CU, -5 % at 2048^3, profiles/r04_f64_ring_ab.log.)
+    const i64 grid_wgs = (m + 127) / 128 * ((n + 127) / 128) * ((kmain + kchunk - 1) / kchunk);
     const int wtm = wtm_env ? wtm_env : ((!ta && tb) || grid_wgs <= 256) ? 32 : 64;
     if (wtm == 64) return launch_shape<Shape<128, 64>>(ta, !tb, p, s);
     return launch_shape<Shape<128>>(ta, !tb, p, s);

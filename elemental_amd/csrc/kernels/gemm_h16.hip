@@ -59,7 +59,7 @@ struct H2Params {
     uint16_t* C; i64 ldc;
     int tiles_m, tiles_n;
     int vec_c;    // C base 8-B aligned and ldc % 4 == 0
-    int group_m;  // tile-order group height (ELX_H16_GROUP, default 4)
+    int group_m;  // tile-order group height (ELX_H16_GROUP, default 8)
 };
 
 __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
@@ -111,19 +111,7 @@ __device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l)
     }
 }
 
-// s_waitcnt through the builtin, not inline asm: hipcc's waitcnt pass sees a
-// builtin wait and drops the conservative waits it would otherwise add for
-// fragment registers whose LDS reads an opaque asm wait already retired (at
-// bf16 TN the asm form left 72 spurious "s_waitcnt lgkmcnt(7)" among the MFMAs
-// of every five K-tiles; removing them: +0.5-2.4 %, bf16 NN 32768^3 1394-1413 ->
-// 1428 TF in one process, profiles/r04_h16_waitcnt_ab.log).  gfx9 encoding: vmcnt [3:0] and [15:14], expcnt
-// [6:4], lgkmcnt [11:8]; the fields not waited on are at their maxima.
-template <int VM, int LGKM>
-__device__ __forceinline__ void wait_cnt() {
-    static_assert(VM >= 0 && VM <= 63 && LGKM >= 0 && LGKM <= 15, "waitcnt field range");
-    __builtin_amdgcn_s_waitcnt((VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (LGKM << 8));
-}
-constexpr int NOWAIT_VM = 63, NOWAIT_LGKM = 15;
+// (wait_cnt: lds_dma.hpp)
 
 __device__ __forceinline__ void bar8() {
     __builtin_amdgcn_sched_barrier(0);
@@ -448,13 +436,16 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-// Tile-order group height: 4, so the 32 concurrent tiles of an XCD span 4 x 8
-// tiles (+1-3 % over 8 x 4 at 32768^3 and 16384^3, profiles/r03_h16_four_wave.log);
-// ELX_H16_GROUP overrides (read per call: A/B tools interleave values), clamped
+// Tile-order group height: 8, so the 32 concurrent tiles of an XCD span 8 x 4
+// tiles.  Round 3 measured 4 ahead by 1-3 % (profiles/r03_h16_four_wave.log); with
+// the round-4 loop (precise waits) 8 is ahead in one process, interleaved: bf16 NN
+// 32768^3 +0.7-2.7 %, f16 +0.3-0.9 %, TN 16384^3 even (profiles/r04_h16_group_ab.log),
+// and reads 106 instead of 131 GB over the fabric per C5 launch, L2 hit 81 vs 77 %
+// (profiles/r04_h16_group_sweep.log).  ELX_H16_GROUP overrides (read per call: A/B tools interleave values), clamped
 // to >= 1 because tile_of divides by it.
 int GroupM() {
     const char* v = getenv("ELX_H16_GROUP");
-    const int g = v ? atoi(v) : 4;
+    const int g = v ? atoi(v) : 8;
     return g >= 1 ? g : 1;
 }
 

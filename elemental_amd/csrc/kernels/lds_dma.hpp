@@ -48,5 +48,28 @@ using DmaSrc = typename std::conditional<BUF, BufferSrc<T>, GlobalSrc<T>>::type;
 // addressed with 31-bit byte offsets from its base?
 inline bool dma_fits(int64_t span, int64_t ld, int64_t es) { return span * ld * es + 16 < (1ll << 31); }
 
+// s_waitcnt through the builtin, not inline asm: hipcc's waitcnt pass sees a
+// builtin wait and drops the conservative waits it would otherwise add for
+// fragment registers whose LDS reads an opaque asm wait already retired (at
+// bf16 TN the asm form left 72 spurious "s_waitcnt lgkmcnt(7)" among the MFMAs
+// of every five K-tiles; removing them: +0.5-2.4 %, bf16 NN 32768^3 1394-1413 ->
+// 1428 TF in one process, profiles/r04_h16_waitcnt_ab.log).  gfx9 encoding: vmcnt [3:0] and [15:14], expcnt
+// [6:4], lgkmcnt [11:8]; the fields not waited on are at their maxima.
+template <int VM, int LGKM>
+__device__ __forceinline__ void wait_cnt() {
+    static_assert(VM >= 0 && VM <= 63 && LGKM >= 0 && LGKM <= 15, "waitcnt field range");
+    __builtin_amdgcn_s_waitcnt((VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (LGKM << 8));
+}
+constexpr int NOWAIT_VM = 63, NOWAIT_LGKM = 15;
+
+// Workgroup barrier without __syncthreads' release fence (which waits for every
+// outstanding vector-memory op, in-flight LDS DMA of later slabs included): the
+// caller's wait_cnt states what must have landed.
+__device__ __forceinline__ void dma_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 }  // namespace kern
 }  // namespace elx

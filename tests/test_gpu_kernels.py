@@ -92,7 +92,8 @@ sys.path.insert(0, sys.argv[1])
 from elemental_amd import _lib as L
 OPS = {"N": 0, "T": 1}
 bad = []
-for (m, n, k) in [(2048, 2048, 2072), (2000, 1990, 1056), (64, 128, 48), (190, 130, 4104)]:
+for (m, n, k) in [(2048, 2048, 2072), (2000, 1990, 1056), (64, 128, 48), (190, 130, 4104), (130, 66, 32),
+                  (66, 130, 16)]:
     for ta in "NT":
         for tb in "NT":
             rng = np.random.default_rng(k + m)
@@ -113,16 +114,17 @@ print("BAD", bad if bad else "none")
 """
 
 
-def test_local_gemm_f64_64row_tiles_exact():
-    """The fp64 LDS-DMA kernel's 64-row tiles (ELX_F64G_BM64: RC images of
-    512-B k-rows, two per DMA instruction), every orientation, edges and the
-    k tail: exact on integer operands (run in a child, the knob is read once)."""
+def test_local_gemm_f64_64x64_tiles_exact():
+    """The fp64 LDS-DMA kernel's 64 x 64 tiles forced on every shape
+    (ELX_F64G_T64=2: RC images of 512-B k-rows, two per DMA instruction, for A
+    and B), every orientation, edges, split-k and the k tail: exact on integer
+    operands (run in a child, the knob is read once)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, "-c", _SMALL_TILE_SCRIPT, root], capture_output=True, text=True,
-                       timeout=110, env=dict(os.environ, ELX_F64G_BM64="100000"))
+                       timeout=110, env=dict(os.environ, ELX_F64G_T64="2"))
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     assert "BAD none" in p.stdout, p.stdout[-2000:]
 
