@@ -38,6 +38,7 @@
 #include <math.h>
 #include <pthread.h>
 #include <stdint.h>
+#include <cpuid.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -222,6 +223,22 @@ static int run_rank(int rank, int n, int nb, int r, int c, int threads, double s
     sh->t_xchg[rank] = R.tx;
     free(R.A); free(R.B); free(R.C0); free(R.C); free(R.A1); free(R.B1);
     return 0;
+}
+
+/* MKL 2021.4 runs its AVX-512 kernels only where it finds an Intel CPU (AVX2
+ * code elsewhere).  The reference's C1 figure was measured on a Xeon (BASELINE.md
+ * §2), i.e. through those kernels; the GPU box's host is an AMD EPYC 9575F (Zen 5,
+ * full AVX-512).  MKL asks this function whether the CPU is Intel's: exported
+ * from the executable (-rdynamic), it is what the dlopen'd MKL binds to, and it
+ * says yes, so the baseline runs the reference's code path on this host too.
+ * CPU_SUMMA_MKL_VENDOR=1 answers from the CPUID vendor string instead (MKL's own
+ * dispatch). */
+int mkl_serv_intel_cpu_true(void) {
+    const char* v = getenv("CPU_SUMMA_MKL_VENDOR");
+    if (!(v && v[0] == '1')) return 1;
+    unsigned a, b, c, d;
+    if (!__get_cpuid(0, &a, &b, &c, &d)) return 0;
+    return b == 0x756e6547u && d == 0x49656e69u && c == 0x6c65746eu; /* "GenuineIntel" */
 }
 
 int main(int argc, char** argv) {
