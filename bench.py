@@ -72,8 +72,11 @@ def cpu_baseline(seconds_target: float = 10.0) -> dict:
     rank pinned to its own): the core count of the reference's own C1 figure
     (0.477 TF on 8 cores), so the two compare per core; the
     same run on every core the box grants (16) is reported beside it.
-    Placement measured on the box (profiles/r04_cpu_baseline_sweep.log):
-    1 / 2 / 4 MKL threads per rank = 69 / 63 / 53 GF per core."""
+    MKL runs its AVX-512 kernels, as on the reference's Xeon (its CPU dispatch
+    would pick its AVX2 code on the box's AMD EPYC 9575F: half the speed; see
+    oracle/cpu_summa.c).  Placement measured on the box
+    (profiles/r04_cpu_baseline_sweep2.log): 1 / 2 / 4 MKL threads per rank =
+    137 / 84 / 107 GF per core with the AVX-512 kernels, 69 / 55 / 52 with AVX2."""
     import oracle
     from oracle import cpu_summa
     out = cpu_summa.run(n=4096, nb=128, r=2, c=2, seconds=seconds_target, cores=8)

@@ -169,7 +169,7 @@ def run_native(n: int, nb: int, r: int, c: int, seconds: float, threads: int) ->
         raise RuntimeError(f"cpu_summa failed ({p.returncode}): {p.stderr[-2000:]}")
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     return {"value": rec["value"], "unit": "TFLOP/s", "cores": threads * world, "kind": "port",
-            "blas": "MKL 2021.4 dgemm_ (the reference's BLAS)",
+            "blas": "MKL 2021.4 dgemm_ (the reference's BLAS), AVX-512 kernels",
             "split_s_per_rank": {"dgemm": rec["gemm_s"], "allgather": rec["exchange_s"], "elapsed": rec["elapsed_s"]},
             "sample": f"C1: CPU SUMMA_NNC NN f64 m=n=k={n}, nb={nb} panels, {r}x{c} grid of {world} forked "
                       f"processes x {threads} MKL threads (oracle/cpu_summa.c: shared-memory all-gathers per "
