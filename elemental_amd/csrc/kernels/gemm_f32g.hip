@@ -28,14 +28,17 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 32, GROUP_M = 8;
-// wave tile WTM x 64: WTM = 32 -> 8 waves (2 x 4 accumulators), 64 -> 4 waves (4 x 4)
-template <int WTM>
-struct WaveShape {
-    static constexpr int MI = WTM / 16, NW = 2 * BM / WTM, NT = 64 * NW;
+constexpr int BK = 32, GROUP_M = 8;
+// Tile BM x BN of waves WTM x WTN: 128 x 128 of 32 x 64 (8 waves, 2 x 4
+// accumulators) or 64 x 64 (4 waves, 4 x 4); 64 x 64 of 32 x 32 (4 waves, 2 x 2)
+// for grids with few 128 x 128 tiles.  Two LDS stages of the two operand images.
+template <int BM_, int BN_, int WTM_, int WTN_>
+struct FShape {
+    static constexpr int BM = BM_, BN = BN_, WTM = WTM_, WTN = WTN_, MI = WTM / 16, NI = WTN / 16;
+    static constexpr int WM = BM / WTM, WN = BN / WTN, NW = WM * WN, NT = 64 * NW;
+    static constexpr int IMGA = BM * BK * 4, IMGB = BN * BK * 4, STAGE = IMGA + IMGB;
+    static constexpr int MINB = BM == 64 && BN == 64 ? 4 : 2;  // workgroups per CU the launch bounds ask for
 };
-constexpr int IMG = 128 * BK * 4;  // 16 KiB per operand image
-constexpr int STAGE = 2 * IMG;
 
 struct FParams {
     i64 m, n, k;  // k: multiple of BK
@@ -65,22 +68,24 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 __device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 5; }
 __device__ __forceinline__ int swz_rc(int kk) { return ((kk >> 3) & 1) << 2; }
 
-// 16 wave-instructions of 1 KiB per image; wave w issues w, w + NW, ...
-template <bool BUF, bool KC, int NW>
+// ROWS / 8 wave-instructions of 1 KiB per image; wave w issues w, w + NW, ...
+template <bool BUF, bool KC, int ROWS, int NW>
 __device__ __forceinline__ void stage_img(const float* X, i64 ld, i64 rows, i64 R, i64 k0, lds_char* img, int w,
                                           int l) {
-    const DmaSrc<BUF, float> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? BM : BK) * ld * 4);
+    static_assert((ROWS / 8) % NW == 0, "image instructions split evenly over the waves");
+    const DmaSrc<BUF, float> src(KC ? X + R * ld + k0 : X + R + k0 * ld, (KC ? ROWS : BK) * ld * 4);
 #pragma unroll
-    for (int q = 0; q < 16 / NW; ++q) {
+    for (int q = 0; q < ROWS / 8 / NW; ++q) {
         const int ins = w + NW * q;
         if (KC) {  // X(row, k) = X[k + row*ld]; 8 rows of 128 B per instruction
             const int r = ins * 8 + (l >> 3);
             const int c = (l & 7) ^ swz_kc(r);
             const i64 row = R + r < rows ? r : rows - 1 - R;
             src.load(row * ld + 4 * c, img + ins * 1024);
-        } else {   // X(row, k) = X[row + k*ld]; 2 k-rows of 512 B per instruction
-            const int kk = ins * 2 + (l >> 5);
-            const int c = (l & 31) ^ swz_rc(kk);
+        } else {   // X(row, k) = X[row + k*ld]; 1024 / (4 ROWS) k-rows of 4 ROWS B per instruction
+            constexpr int CPK = ROWS / 4, KPI = 64 / CPK;  // 16-B chunks per k-row, k-rows per instruction
+            const int kk = ins * KPI + l / CPK;
+            const int c = (l % CPK) ^ swz_rc(kk);
             const i64 col = R + 4 * c <= rows - 4 ? 4 * c : rows - 4 - R;
             src.load(col + kk * ld, img + ins * 1024);
         }
@@ -88,7 +93,7 @@ __device__ __forceinline__ void stage_img(const float* X, i64 ld, i64 rows, i64 
 }
 
 // The slab's 8 operand values of one 16-row fragment: element s = X(R0 + (l&15), 8(l>>4) + s).
-template <bool KC>
+template <bool KC, int ROWS>
 __device__ __forceinline__ void frag(const lds_char* img, int R0, int l, float (&v)[8]) {
     const int r = R0 + (l & 15), g = l >> 4;
     if (KC) {
@@ -103,7 +108,7 @@ __device__ __forceinline__ void frag(const lds_char* img, int R0, int l, float (
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const int kk = 8 * g + s;
-            const int off = kk * 512 + (((r >> 2) ^ swz_rc(kk)) << 4) + ((r & 3) << 2);
+            const int off = kk * (ROWS * 4) + (((r >> 2) ^ swz_rc(kk)) << 4) + ((r & 3) << 2);
             v[s] = *(const __attribute__((address_space(3))) float*)(img + off);
         }
     }
@@ -117,37 +122,36 @@ struct Frame {
 
 // __restrict__ LDS pointers: alias scopes so the in-flight DMA is not drained
 // before the ds_reads (see gemm_h256.hip).
-template <int WTM, bool KCA, bool KCB, bool BUF>
+template <typename SH, bool KCA, bool KCB, bool BUF>
 __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_char* __restrict__ next,
-                                     const lds_char* __restrict__ cur, f32x4 (&acc)[WTM / 16][4]) {
-    using WS = WaveShape<WTM>;
+                                     const lds_char* __restrict__ cur, f32x4 (&acc)[SH::MI][SH::NI]) {
     if (more) {
-        stage_img<BUF, KCA, WS::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
-        stage_img<BUF, KCB, WS::NW>(f.B, f.ldb, f.n, f.n0, knext, next + IMG, f.w, f.l);
+        stage_img<BUF, KCA, SH::BM, SH::NW>(f.A, f.lda, f.m, f.m0, knext, next, f.w, f.l);
+        stage_img<BUF, KCB, SH::BN, SH::NW>(f.B, f.ldb, f.n, f.n0, knext, next + SH::IMGA, f.w, f.l);
     }
-    float a[WS::MI][8], b[4][8];
+    float a[SH::MI][8], b[SH::NI][8];
 #pragma unroll
-    for (int mi = 0; mi < WS::MI; ++mi) frag<KCA>(cur, f.wr * WTM + mi * 16, f.l, a[mi]);
+    for (int mi = 0; mi < SH::MI; ++mi) frag<KCA, SH::BM>(cur, f.wr * SH::WTM + mi * 16, f.l, a[mi]);
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) frag<KCB>(cur + IMG, f.wc * 64 + ni * 16, f.l, b[ni]);
+    for (int ni = 0; ni < SH::NI; ++ni) frag<KCB, SH::BN>(cur + SH::IMGA, f.wc * SH::WTN + ni * 16, f.l, b[ni]);
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int mi = 0; mi < WS::MI; ++mi)
+        for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < SH::NI; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi][s], b[ni][s], acc[mi][ni], 0, 0, 0);
 }
 
 // BUF: staging through buffer descriptors (lds_dma.hpp) where the offsets fit.
-template <int WTM, bool KCA, bool KCB, bool BETA0, bool BUF>
-__global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParams p) {
-    using WS = WaveShape<WTM>;
+template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f32g_kernel(FParams p) {
+    constexpr int BM = SH::BM, BN = SH::BN, STAGE = SH::STAGE;
     __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;  // BM/WTM (M) x 2 (N) waves of WTM x 64
+    const int wr = w / SH::WN, wc = w % SH::WN;  // WM (M) x WN (N) waves of WTM x WTN
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
@@ -160,41 +164,41 @@ __global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParam
     }
     const Frame f{p.A, p.lda, p.m, m0, p.B, p.ldb, p.n, n0, w, l, wr, wc};
 
-    f32x4 acc[WS::MI][4];
+    f32x4 acc[SH::MI][SH::NI];
 #pragma unroll
-    for (int a = 0; a < WS::MI; ++a)
+    for (int a = 0; a < SH::MI; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+        for (int b = 0; b < SH::NI; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<BUF, KCA, WS::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<BUF, KCB, WS::NW>(p.B, p.ldb, p.n, n0, 0, lds + IMG, w, l);
+    stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+    stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         const int cur = t & 1;
-        slab<WTM, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 
     // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
     const int g = l >> 4, c = l & 15;
-    const i64 ib = m0 + wr * WTM + 4 * g, jb = n0 + wc * 64 + c;
+    const i64 ib = m0 + wr * SH::WTM + 4 * g, jb = n0 + wc * SH::WTN + c;
     if (p.vec_c && m0 + BM <= p.m && n0 + BN <= p.n) {
         // interior tile: a 16-row block's C loads all issued before its first
         // store (the guarded form below serializes load -> wait -> store per
         // element, since the compiler cannot reorder loads across the stores)
 #pragma unroll
-        for (int mi = 0; mi < WS::MI; ++mi) {
-            f32x4 cv[4];
+        for (int mi = 0; mi < SH::MI; ++mi) {
+            f32x4 cv[SH::NI];
             if (!BETA0) {
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < SH::NI; ++ni)
                     cv[ni] = *reinterpret_cast<const f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16);
             }
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
+            for (int ni = 0; ni < SH::NI; ++ni) {
                 f32x4 v = p.alpha * acc[mi][ni];
                 if (!BETA0) v += p.beta * cv[ni];
                 *reinterpret_cast<f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16) = v;
@@ -203,9 +207,9 @@ __global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParam
         return;
     }
 #pragma unroll
-    for (int mi = 0; mi < WS::MI; ++mi)
+    for (int mi = 0; mi < SH::MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
+        for (int ni = 0; ni < SH::NI; ++ni) {
             const i64 j = jb + ni * 16;
             if (j >= p.n) continue;
             float* col = p.C + j * p.ldc;
@@ -220,13 +224,23 @@ __global__ __launch_bounds__(WaveShape<WTM>::NT, 2) void gemm_f32g_kernel(FParam
         }
 }
 
-template <int WTM, bool KCA, bool KCB, bool BUF>
-hipError_t launch_fw(const FParams& p, hipStream_t s) {
+template <typename SH, bool KCA, bool KCB, bool BUF>
+hipError_t launch_fw(FParams p, hipStream_t s) {
+    p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
+    p.tiles_n = (int)((p.n + SH::BN - 1) / SH::BN);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    const dim3 block(WaveShape<WTM>::NT);
-    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<WTM, KCA, KCB, true, BUF>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((gemm_f32g_kernel<WTM, KCA, KCB, false, BUF>), grid, block, 0, s, p);
+    const dim3 block(SH::NT);
+    if (p.beta == 0.f) hipLaunchKernelGGL((gemm_f32g_kernel<SH, KCA, KCB, true, BUF>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemm_f32g_kernel<SH, KCA, KCB, false, BUF>), grid, block, 0, s, p);
     return hipGetLastError();
+}
+
+// 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU, whole k) where
+// prefer_t64 (kernels.hpp) says they balance the CUs better; ELX_F32G_T64 = 0
+// never, 2 always (tests).
+bool t64_tiles(i64 m, i64 n) {
+    static const int v = [] { const char* e = getenv("ELX_F32G_T64"); return e ? atoi(e) : 1; }();
+    return prefer_t64(v, m, n);
 }
 
 template <bool KCA, bool KCB, bool BUF>
@@ -239,14 +253,15 @@ hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // profiles/r03_f32_wtm.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
-    if (wtm == 64) return launch_fw<64, KCA, KCB, BUF>(p, s);
-    return launch_fw<32, KCA, KCB, BUF>(p, s);
+    if (t64_tiles(p.m, p.n)) return launch_fw<FShape<64, 64, 32, 32>, KCA, KCB, BUF>(p, s);
+    if (wtm == 64) return launch_fw<FShape<128, 128, 64, 64>, KCA, KCB, BUF>(p, s);
+    return launch_fw<FShape<128, 128, 32, 64>, KCA, KCB, BUF>(p, s);
 }
 
 template <bool KCA, bool KCB>
 hipError_t launch_f(const FParams& p, hipStream_t s) {
     static const bool global_only = [] { const char* v = getenv("ELX_F32G_STAGE"); return v && v[0] == 'g'; }();
-    if (!global_only && dma_fits(KCA ? BM : BK, p.lda, 4) && dma_fits(KCB ? BN : BK, p.ldb, 4))
+    if (!global_only && dma_fits(KCA ? 128 : BK, p.lda, 4) && dma_fits(KCB ? 128 : BK, p.ldb, 4))
         return launch_fb<KCA, KCB, true>(p, s);
     return launch_fb<KCA, KCB, false>(p, s);
 }
@@ -260,13 +275,13 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 4 == 0 && ldb % 4 == 0 && (kca || (m % 4 == 0 && m >= 4)) &&
                     (kcb || (n % 4 == 0 && n >= 4)) && m < (1ll << 31) && n < (1ll << 31);
-    return dma_plan(ok, (m + BM - 1) / BM * ((n + BN - 1) / BN), k, BK);
+    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
+    return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 
 hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
                             i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s) {
-    FParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-              kchunk, m * n, (reinterpret_cast<uintptr_t>(C) & 15) == 0 && ldc % 4 == 0 && (kchunk >= kmain || m % 4 == 0)};
+    FParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0, kchunk, m * n, (reinterpret_cast<uintptr_t>(C) & 15) == 0 && ldc % 4 == 0 && (kchunk >= kmain || m % 4 == 0)};
     const bool kca = ta, kcb = !tb;
     if (kca) return kcb ? launch_f<true, true>(p, s) : launch_f<true, false>(p, s);
     return kcb ? launch_f<false, true>(p, s) : launch_f<false, false>(p, s);

@@ -276,18 +276,12 @@ hipError_t launch_shape(bool kca, bool kcb, const GParams& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-// 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU) for grids with
-// fewer than two 128 x 128 tiles per CU but at least two 64 x 64 ones, whole k
-// (no split-k partials); ELX_F64G_T64 = 0 never, 2 always (tests).
-int t64_mode() {
-    static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
-    return v;
-}
+// 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU, whole k) where
+// prefer_t64 (kernels.hpp) says they balance the CUs better; ELX_F64G_T64 = 0
+// never, 2 always (tests).
 bool t64_tiles(i64 m, i64 n) {
-    const int mode = t64_mode();
-    if (mode != 1) return mode == 2;
-    const i64 t128 = (m + 127) / 128 * ((n + 127) / 128), t64 = (m + 63) / 64 * ((n + 63) / 64);
-    return t128 < 512 && t64 >= 512;
+    static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
+    return prefer_t64(v, m, n);
 }
 
 }  // namespace

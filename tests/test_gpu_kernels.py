@@ -90,21 +90,22 @@ _SMALL_TILE_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, sys.argv[1])
 from elemental_amd import _lib as L
+dt = np.float64 if sys.argv[2] == "f64" else np.float32
 OPS = {"N": 0, "T": 1}
 bad = []
-for (m, n, k) in [(2048, 2048, 2072), (2000, 1990, 1056), (64, 128, 48), (190, 130, 4104), (130, 66, 32),
-                  (66, 130, 16)]:
+for (m, n, k) in [(2048, 2048, 2072), (2000, 1990, 1056), (64, 128, 48), (190, 130, 4104), (132, 68, 32),
+                  (68, 132, 64)]:
     for ta in "NT":
         for tb in "NT":
             rng = np.random.default_rng(k + m)
-            A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
-            B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(np.float64))
-            C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(np.float64))
+            A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(dt))
+            B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(dt))
+            C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(dt))
             dv = lambda X: torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
             dA, dB, dC = dv(A), dv(B), dv(C)
             torch.cuda.synchronize()
-            L.call("elx_gemm_f64", OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0], dB.data_ptr(),
-                   B.shape[0], -1.0, dC.data_ptr(), m, None)
+            L.call("elx_gemm_" + sys.argv[2], OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0],
+                   dB.data_ptr(), B.shape[0], -1.0, dC.data_ptr(), m, None)
             L.call("elx_device_synchronize")
             got = dC.cpu().numpy().T
             want = 2.0 * (A if ta == "N" else A.T) @ (B if tb == "N" else B.T) - C
@@ -114,17 +115,19 @@ print("BAD", bad if bad else "none")
 """
 
 
-def test_local_gemm_f64_64x64_tiles_exact():
-    """The fp64 LDS-DMA kernel's 64 x 64 tiles forced on every shape
-    (ELX_F64G_T64=2: RC images of 512-B k-rows, two per DMA instruction, for A
-    and B), every orientation, edges, split-k and the k tail: exact on integer
-    operands (run in a child, the knob is read once)."""
+@pytest.mark.parametrize("dtype,knob", [("f64", "ELX_F64G_T64"), ("f32", "ELX_F32G_T64")])
+def test_local_gemm_64x64_tiles_exact(dtype, knob):
+    """The LDS-DMA kernels' 64 x 64 tiles forced on every shape (ELX_F64G_T64=2 /
+    ELX_F32G_T64=2: RC images of 512-B (fp64) / 256-B (fp32) k-rows, several per
+    DMA instruction, for A and B), every orientation, edges, split-k and the k
+    tail: exact on small-integer operands (products and sums stay exact in fp32
+    too), run in a child since the knob is read once."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, "-c", _SMALL_TILE_SCRIPT, root], capture_output=True, text=True,
-                       timeout=110, env=dict(os.environ, ELX_F64G_T64="2"))
+    p = subprocess.run([sys.executable, "-c", _SMALL_TILE_SCRIPT, root, dtype], capture_output=True, text=True,
+                       timeout=110, env=dict(os.environ, **{knob: "2"}))
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     assert "BAD none" in p.stdout, p.stdout[-2000:]
 
