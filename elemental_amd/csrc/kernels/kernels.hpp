@@ -65,18 +65,22 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
     d.nz = (int)((d.kmain + d.kchunk - 1) / d.kchunk);
     return d;
 }
-// 128 x 128 or 64 x 64 tiles for the LDS-DMA kernels (fp64 and fp32): the tile
-// count per CU rounds up to whole tiles, so a grid leaves CUs idle in its last
-// round unless its tile count is a multiple of 256.  64 x 64 tiles (four per CU
-// in flight, ~5 % slower per FLOP than 128 x 128 where both fill the chip:
-// profiles/r04_t64_rule_ab.log) win when their balance beats the 128-tile one by
-// more than that: 1536 x 2048 (192 vs 768 tiles), 2560^2, 3072^2 (576 vs 2304:
-// fp64 51.8 -> 67.0 TF, fp32 109 -> 132), 3584^2; not 2048^2, 4096^2 or any other
-// multiple of 256 128-tiles.  mode: 0 never, 2 always (tests), else this rule.
+// 128 x 128 or 64 x 64 tiles for the LDS-DMA kernels (fp64 and fp32).  Grids
+// of fewer 128-tiles than CUs take 64 x 64 tiles (four times the workgroups,
+// with dma_plan's split-k on that count): 1024^3 fp32 69 -> 93 TF, fp64 38 -> 46;
+// 512^2 x 2048 fp32 37 -> 52; 1024^2 x 2048 even (profiles/r04_small_t64_ab.log).
+// Above that, the tile count per CU rounds up to whole tiles, so a grid leaves
+// CUs idle in its last round unless its tile count is a multiple of 256; 64 x 64
+// tiles (four per CU in flight, ~5 % slower per FLOP than 128 x 128 where both
+// fill the chip: profiles/r04_t64_rule_ab.log) win when their balance beats the
+// 128-tile one by more than that: 1536 x 2048 (192 vs 768 tiles), 2560^2, 3072^2
+// (576 vs 2304: fp64 51.8 -> 67.0 TF, fp32 109 -> 132), 3584^2; not 2048^2,
+// 4096^2 or any other multiple of 256 128-tiles.  mode: 0 never, 2 always
+// (tests), else this rule.
 inline bool prefer_t64(int mode, i64 m, i64 n) {
     if (mode == 0 || mode == 2) return mode == 2;
     const i64 t128 = (m + 127) / 128 * ((n + 127) / 128), t64 = (m + 63) / 64 * ((n + 63) / 64);
-    if (t64 < 512) return false;
+    if (t128 < 256) return true;
     const auto bal = [](i64 t) { return (double)t / (double)(256 * ((t + 255) / 256)); };
     return 0.95 * bal(t64) > bal(t128);
 }
