@@ -281,7 +281,7 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 // never, 2 always (tests).
 bool t64_tiles(i64 m, i64 n) {
     static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
-    return prefer_t64(v, m, n);
+    return prefer_t64(v, m, n, 256);
 }
 
 }  // namespace
@@ -306,7 +306,16 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     }();
     static const int rm = [] { const char* v = getenv("ELX_F64G_REMAP"); return v ? atoi(v) : 1; }();
     GParams p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, 0, 0, kchunk, m * n, gm, rm};
-    if (t64_tiles(m, n)) return launch_shape<Shape<64, 32, BK, 64, 32>>(ta, !tb, p, s);
+    // 64 x 64 tiles: eight waves of 32 x 16 where A is rows-contiguous (NN / NT:
+    // 2048^3 NN 64.4 -> 66.2 TF, 1536 x 2048^2 62.5 -> 64.6, 1024^2 x 2048 49.9 ->
+    // 54.8), four of 32 x 32 where it is k-contiguous (TN 64.4 vs 60.3 with eight,
+    // TT 65.0 vs 62.2); profiles/r04_t64_waves8_ab.log (the fp32 kernel measured
+    // 4-13 % slower with eight and keeps four).  ELX_F64G_T64W = 4 / 8 forces one.
+    static const int t64w = [] { const char* v = getenv("ELX_F64G_T64W"); return v ? atoi(v) : 0; }();
+    if (t64_tiles(m, n)) {
+        if (t64w == 8 || (t64w != 4 && !ta)) return launch_shape<Shape<64, 32, BK, 64, 16>>(ta, !tb, p, s);
+        return launch_shape<Shape<64, 32, BK, 64, 32>>(ta, !tb, p, s);
+    }
     // wave tile: 64 x 64 (four waves) measured +1.5-2 % for NN/TN/TT; NT (both
     // operands rows-contiguous) runs faster with 32 x 64 (profiles/r01_f64_wave.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F64G_WTM"); return v ? atoi(v) : 0; }();

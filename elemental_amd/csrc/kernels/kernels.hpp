@@ -76,11 +76,14 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
 // 128-tile one by more than that: 1536 x 2048 (192 vs 768 tiles), 2560^2, 3072^2
 // (576 vs 2304: fp64 51.8 -> 67.0 TF, fp32 109 -> 132), 3584^2; not 2048^2,
 // 4096^2 or any other multiple of 256 128-tiles.  mode: 0 never, 2 always
-// (tests), else this rule.
-inline bool prefer_t64(int mode, i64 m, i64 n) {
+// (tests), else this rule.  small: the largest 128-tile count that always takes
+// 64 x 64 tiles (fp32 255; fp64 256, where its eight-wave 64 x 64 tiles beat the
+// one-workgroup-per-CU 128 x 128 grid at 2048^2 in every orientation: NN 64.0 ->
+// 66.2 TF, profiles/r04_t64_waves8_ab.log).
+inline bool prefer_t64(int mode, i64 m, i64 n, i64 small = 255) {
     if (mode == 0 || mode == 2) return mode == 2;
     const i64 t128 = (m + 127) / 128 * ((n + 127) / 128), t64 = (m + 63) / 64 * ((n + 63) / 64);
-    if (t128 < 256) return true;
+    if (t128 <= small) return true;
     const auto bal = [](i64 t) { return (double)t / (double)(256 * ((t + 255) / 256)); };
     return 0.95 * bal(t64) > bal(t128);
 }
