@@ -32,12 +32,17 @@ constexpr int BK = 32, GROUP_M = 8;
 // Tile BM x BN of waves WTM x WTN: 128 x 128 of 32 x 64 (8 waves, 2 x 4
 // accumulators) or 64 x 64 (4 waves, 4 x 4); 64 x 64 of 32 x 32 (4 waves, 2 x 2)
 // for grids with few 128 x 128 tiles.  Two LDS stages of the two operand images.
-template <int BM_, int BN_, int WTM_, int WTN_>
+// NST_ > 2: an LDS ring of NST_ slabs (the next NST_ - 1 in flight) for grids of
+// at most one workgroup per CU, where one slab of lead is shorter than the DMA's
+// latency.
+template <int BM_, int BN_, int WTM_, int WTN_, int NST_ = 2>
 struct FShape {
     static constexpr int BM = BM_, BN = BN_, WTM = WTM_, WTN = WTN_, MI = WTM / 16, NI = WTN / 16;
-    static constexpr int WM = BM / WTM, WN = BN / WTN, NW = WM * WN, NT = 64 * NW;
+    static constexpr int WM = BM / WTM, WN = BN / WTN, NW = WM * WN, NT = 64 * NW, NST = NST_;
     static constexpr int IMGA = BM * BK * 4, IMGB = BN * BK * 4, STAGE = IMGA + IMGB;
-    static constexpr int MINB = BM == 64 && BN == 64 ? 4 : 2;  // workgroups per CU the launch bounds ask for
+    static constexpr int IPS = STAGE / 1024 / NW;  // DMA instructions per wave and slab (the ring's vmcnt unit)
+    static constexpr int MINB = NST_ > 2 ? 1 : BM == 64 && BN == 64 ? 4 : 2;  // workgroups per CU the launch bounds ask for
+    static_assert((NST_ - 1) * IPS <= 63 && NST_ * STAGE <= 160 * 1024, "ring depth");
 };
 
 struct FParams {
@@ -147,7 +152,7 @@ __device__ __forceinline__ void slab(const Frame& f, i64 knext, bool more, lds_c
 template <typename SH, bool KCA, bool KCB, bool BETA0, bool BUF>
 __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f32g_kernel(FParams p) {
     constexpr int BM = SH::BM, BN = SH::BN, STAGE = SH::STAGE;
-    __shared__ __attribute__((aligned(1024))) char lds_raw[2 * STAGE];
+    __shared__ __attribute__((aligned(1024))) char lds_raw[SH::NST * STAGE];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -171,15 +176,45 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f32g_kernel(FParams p) 
         for (int b = 0; b < SH::NI; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
-    stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
-    stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-        const int cur = t & 1;
-        slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE, acc);
+    if constexpr (SH::NST == 2) {
+        stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, 0, lds, w, l);
+        stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, 0, lds + SH::IMGA, w, l);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        for (int t = 0; t < nt; ++t) {
+            const int cur = t & 1;
+            slab<SH, KCA, KCB, BUF>(f, (i64)(t + 1) * BK, t + 1 < nt, lds + (cur ^ 1) * STAGE, lds + cur * STAGE,
+                                    acc);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        // ring: slabs t+1 .. t+AHEAD in flight while slab t computes; slab t+AHEAD
+        // goes into the stage slab t-1 left (every wave passed the barrier after
+        // it).  Barriers without __syncthreads' fence, which would drain the ring.
+        constexpr int AHEAD = SH::NST - 1;
+#pragma unroll
+        for (int q = 0; q < AHEAD; ++q) {
+            if (q < nt) {
+                stage_img<BUF, KCA, BM, SH::NW>(p.A, p.lda, p.m, m0, (i64)q * BK, lds + q * STAGE, w, l);
+                stage_img<BUF, KCB, BN, SH::NW>(p.B, p.ldb, p.n, n0, (i64)q * BK, lds + q * STAGE + SH::IMGA, w, l);
+            }
+        }
+        if (nt >= AHEAD) wait_cnt<(AHEAD - 1) * SH::IPS, NOWAIT_LGKM>();  // slab 0 landed
+        else wait_cnt<0, NOWAIT_LGKM>();
+        dma_barrier();
+        int cur = 0, nxt = AHEAD;  // stages of slab t and of slab t + AHEAD
+        for (int t = 0; t < nt; ++t) {
+            slab<SH, KCA, KCB, BUF>(f, (i64)(t + AHEAD) * BK, t + AHEAD < nt, lds + nxt * STAGE, lds + cur * STAGE,
+                                    acc);
+            // slab t+1 landed (the AHEAD-1 younger slabs may fly; near the end
+            // drain fully) and this wave's reads of slab t retired
+            if (t + AHEAD < nt) wait_cnt<(AHEAD - 1) * SH::IPS, 0>();
+            else wait_cnt<0, 0>();
+            dma_barrier();
+            cur = cur + 1 == SH::NST ? 0 : cur + 1;
+            nxt = nxt + 1 == SH::NST ? 0 : nxt + 1;
+        }
     }
 
     // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
@@ -253,7 +288,14 @@ hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // profiles/r03_f32_wtm.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
-    if (t64_tiles(p.m, p.n)) return launch_fw<FShape<64, 64, 32, 32>, KCA, KCB, BUF>(p, s);
+    if (t64_tiles(p.m, p.n)) {
+        // at most one workgroup per CU: a 4-slab LDS ring unless NN (NT 1024^2 x
+        // 2048 72.7 -> 93.7 TF, TN 96.4 -> 99.8, NN even; the fp64 kernel lost
+        // with it; profiles/r04_small_ring_ab.log)
+        const i64 wgs = (p.m + 63) / 64 * ((p.n + 63) / 64) * ((p.k + p.kchunk - 1) / p.kchunk);
+        if (wgs <= 256 && (KCA || !KCB)) return launch_fw<FShape<64, 64, 32, 32, 4>, KCA, KCB, BUF>(p, s);
+        return launch_fw<FShape<64, 64, 32, 32>, KCA, KCB, BUF>(p, s);
+    }
     if (wtm == 64) return launch_fw<FShape<128, 128, 64, 64>, KCA, KCB, BUF>(p, s);
     return launch_fw<FShape<128, 128, 32, 64>, KCA, KCB, BUF>(p, s);
 }
