@@ -28,6 +28,7 @@
 // measurements are in profiles/r01_gemm16_h256.log, r01_h16_ablation.log,
 // r02_h16_deep.log and r03_h16_four_wave.log (the four-wave kernel beat each).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <utility>
@@ -60,6 +61,11 @@ struct H2Params {
     int tiles_m, tiles_n;
     int vec_c;    // C base 8-B aligned and ldc % 4 == 0
     int group_m;  // tile-order group height (ELX_H16_GROUP, default 8)
+    // split-k (gridDim.y chunks, W != null): chunk z covers k in [z*kchunk,
+    // min(k, (z+1)*kchunk)) and writes its raw f32 product to W + z*m*n (ld m);
+    // h16_splitk_reduce applies alpha / beta and rounds once
+    i64 kchunk;
+    float* W;
 };
 
 __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
@@ -260,6 +266,45 @@ __device__ __forceinline__ void settle(f32x4 (&acc)[8][8]) {
         for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
 }
 
+// Split-k partial of one wave: the raw f32 accumulators into W (ld m)
+__device__ __forceinline__ void epilogue_partial(const H2Params& p, const f32x4 (&acc)[8][8], i64 m0, i64 n0, int wr,
+                                                 int wc, int l) {
+    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 128 + (l & 15);
+    const bool vec = (p.m & 3) == 0;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const i64 i = rb + mi * 16, j = cb + ni * 16;
+            if (j >= p.n || i >= p.m) continue;
+            float* o = p.W + i + j * p.m;
+            if (vec) {
+                *reinterpret_cast<f32x4*>(o) = acc[mi][ni];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (i + r < p.m) o[r] = acc[mi][ni][r];
+            }
+        }
+}
+
+// C = alpha sum_z W_z + beta C, rounded once to the 16-bit type
+template <bool BF16>
+__global__ __launch_bounds__(256) void h16_splitk_reduce(i64 m, i64 n, int nz, float alpha, const float* __restrict__ W,
+                                                         float beta, uint16_t* __restrict__ C, i64 ldc) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    const i64 mn = m * n;
+    for (i64 e = (i64)blockIdx.x * 256 + threadIdx.x; e < mn; e += (i64)gridDim.x * 256) {
+        float v = 0.f;
+        for (int z = 0; z < nz; ++z) v += W[z * mn + e];
+        const i64 i = e % m, j = e / m;
+        uint16_t* o = C + i + j * ldc;
+        v *= alpha;
+        if (beta != 0.f) v += beta * E::load(*o);
+        *o = E::store(v);
+    }
+}
+
 // C tile of one wave (128 x 128): accumulator (mi, ni) holds rows
 // rb + 16 mi + 4 (l >> 4) + {0..3}, column cb + 16 ni + (l & 15).  One row of
 // accumulators at a time (C loads, then stores), so at most 32 values live in
@@ -341,7 +386,9 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 }
 }  // namespace w4
 
-template <bool BF16, bool KCA, bool KCB, bool BUF>
+// PART: split-k partials (p.W, gridDim.y chunks), a separate instantiation so the
+// default kernel's epilogue keeps its register allocation
+template <bool BF16, bool KCA, bool KCB, bool BUF, bool PART>
 __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
@@ -353,6 +400,13 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
     const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    if constexpr (PART) {  // this workgroup's k chunk
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += KCA ? kz0 : kz0 * p.lda;
+        p.B += KCB ? kz0 : kz0 * p.ldb;
+        p.W += (i64)blockIdx.y * p.m * p.n;
+    }
 
     Pieces pc;
 #pragma unroll
@@ -415,7 +469,8 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
     w4::settle(acc);
-    w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
+    if constexpr (PART) w4::epilogue_partial(p, acc, m0, n0, wr, wc, l);
+    else w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
 }
 
 // (Measured and removed in round 4: a two-barrier loop that keeps every wave's
@@ -428,9 +483,14 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
     // buffer-descriptor DMA when every offset of an image fits 31 bits, else the
     // global (64-bit address) form
     const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
-    const dim3 grid(p.tiles_m * p.tiles_n);
-    if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false>), grid, dim3(256), 0, s, p);
+    const dim3 grid(p.tiles_m * p.tiles_n, p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
+    if (p.W) {
+        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
+    } else {
+        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
+    }
     return hipGetLastError();
 }
 
@@ -458,19 +518,54 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     const i64 kmain = k / BK * BK;
     // the large-tile path: 16-B aligned rows/columns for the DMA, RC operands a
     // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
+    const i64 tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
+    // split-k where the tiles leave at least half the CUs idle: chunks of >= 4
+    // K-tiles, up to one workgroup per CU; f32 partials in the stream-ordered
+    // workspace, one reduce that applies alpha / beta and rounds once.  bf16
+    // 1024^2 x 8192 41 -> 350 TF, 2048^2 x 8192 481 -> 866, 1024^3 32 -> 69, 2048^3
+    // 326 -> 360; at 3072^2 (144 tiles) two chunks lost 35 %, so it stays whole
+    // (profiles/r04_h16_split_ab.log).  ELX_H16_SPLIT=0 disables.
+    static const bool split_on = [] { const char* v = getenv("ELX_H16_SPLIT"); return !v || v[0] != '0'; }();
+    i64 nz = 1, kchunk = kmain;
+    if (split_on && tiles <= 128 && kmain >= 8 * BK) {
+        const i64 z = std::min<i64>((256 + tiles - 1) / tiles, kmain / (4 * BK));
+        if (z >= 2) {
+            kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
+            nz = (kmain + kchunk - 1) / kchunk;
+        }
+    }
     const bool ok = kmain > 0 && al16(A) && al16(B) && lda % 8 == 0 && ldb % 8 == 0 &&
-                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) &&
-                    ((m + BM - 1) / BM) * ((n + BN - 1) / BN) >= 64 && m < (1ll << 31) && n < (1ll << 31);
+                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) && tiles * nz >= 64 &&
+                    m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM()};
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), kchunk, nullptr};
     hipError_t e;
+    if (nz > 1) {
+        e = workspace_alloc(reinterpret_cast<void**>(&p.W), sizeof(float) * (size_t)m * (size_t)n * (size_t)nz, s);
+        if (e != hipSuccess) return e;
+    }
     if (is_bf16) {
         if (kca) e = kcb ? launch_h16<true, true, true>(p, s) : launch_h16<true, true, false>(p, s);
         else e = kcb ? launch_h16<true, false, true>(p, s) : launch_h16<true, false, false>(p, s);
     } else {
         if (kca) e = kcb ? launch_h16<false, true, true>(p, s) : launch_h16<false, true, false>(p, s);
         else e = kcb ? launch_h16<false, false, true>(p, s) : launch_h16<false, false, false>(p, s);
+    }
+    if (nz > 1) {
+        if (e == hipSuccess) {
+            const i64 mn = m * n;
+            const unsigned grid = (unsigned)std::min<i64>((mn + 255) / 256, 2048);
+            if (is_bf16)
+                hipLaunchKernelGGL((w4::h16_splitk_reduce<true>), dim3(grid), dim3(256), 0, s, m, n, (int)nz, alpha, p.W,
+                                   beta, C, ldc);
+            else
+                hipLaunchKernelGGL((w4::h16_splitk_reduce<false>), dim3(grid), dim3(256), 0, s, m, n, (int)nz, alpha, p.W,
+                                   beta, C, ldc);
+            e = hipGetLastError();
+        }
+        const hipError_t f = workspace_free(p.W, s);
+        if (e == hipSuccess) e = f;
     }
     if (e != hipSuccess || kmain == k) return e;
     // k tail (< 64): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
