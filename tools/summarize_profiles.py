@@ -41,8 +41,8 @@ if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     res["note"] = "FETCH_SIZE x2 (gfx950 counts half of wide streaming reads) + WRITE_SIZE, KB -> bytes"
 if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
     res["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-# MFMA utilisation from the calibrated MOPS counter (tools/pmc_metrics.py: the
-# SQ_VALU_MFMA_BUSY_CYCLES reading of rounds 1-3 was a pegged constant)
+# MFMA utilisation from the calibrated MOPS counter, cross-checked by
+# SQ_VALU_MFMA_BUSY_CYCLES (both exact: tools/pmc_metrics.py, profiles/r04_mfma_calib.log)
 dtype = key.split(":")[0]
 secs = None
 if stats and exact:
