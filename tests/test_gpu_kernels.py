@@ -193,6 +193,36 @@ def test_local_gemm_16bit(kind, ta, tb, shape):
 
 
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
+@pytest.mark.parametrize("alpha,beta", [(0.5, 0.0), (-1.0, 0.25)])
+def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
+    """The 16-bit split-k reduce applies alpha and beta (including beta = 0, where
+    C is not read: it holds NaN here) once, after summing the f32 partials:
+    integer operands keep every partial and the scaled sum exact, so the result
+    is numpy's single rounding of the exact value, bit for bit."""
+    m, n, k = 1024, 1024, 8192
+    rng = np.random.default_rng(7)
+    A = rng.integers(-2, 3, (m, k)).astype(np.float32)
+    B = rng.integers(-2, 3, (k, n)).astype(np.float32)
+    C = rng.integers(-64, 65, (m, n)).astype(np.float32)
+    if beta == 0.0:
+        C[:] = np.nan
+    exact = alpha * (A.astype(np.float64) @ B.astype(np.float64)) + (beta * C.astype(np.float64) if beta else 0.0)
+    if kind == "f16":
+        enc = lambda x: np.asfortranarray(x.astype(np.float16))
+        fn, want = L.lib().elx_gemm_f16, exact.astype(np.float16).view(np.uint16)
+    else:
+        enc = lambda x: np.asfortranarray(oracle.f32_to_bf16_bits(x))
+        fn, want = L.lib().elx_gemm_bf16, oracle.f32_to_bf16_bits(exact.astype(np.float32))
+    dA, dB, dC = dev(enc(A)), dev(enc(B)), dev(enc(C))
+    torch.cuda.synchronize()
+    L.check(fn(0, 0, m, n, k, alpha, dA.data_ptr(), m, dB.data_ptr(), k, beta, dC.data_ptr(), m, None))
+    sync()
+    got = host(dC, (m, n), np.uint16)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, f"{kind} alpha={alpha} beta={beta}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
+
+
+@pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64), (1024, 1024, 8192),
