@@ -226,18 +226,18 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64), (1024, 1024, 8192),
-                                   (1002, 1032, 4096)])
+                                   (1002, 1032, 4096), (2048, 2048, 2112), (1536, 2312, 704)])
 def test_local_gemm_16bit_exact(kind, ta, tb, shape):
     """Integer operands in [-2, 2]: every partial sum is exact in the f32
     accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
     to 16 bits, and the result must equal numpy's rounding of the exact value bit
     for bit.  k = 2112: 66 slabs of 32 (the 16-bit kernels' main loop over many
     wraps of their LDS ring); 2312 columns: ragged edge tiles; k = 64: a single
-    K-tile (the ring's prologue and clamped restaging only).  Grids of fewer
-    256-tiles than CUs split k (f32 partials, one reduce that rounds once):
-    (2048, 2312, 2112) 4 chunks, (4096, 2048, 640) 2, (1024, 1024, 8192) 16,
-    (1002, 1032, 4096) with m % 4 != 0 (the partials' scalar stores; TN / TT only,
-    the others take the 128 x 128 kernel).  (k a multiple of 64: a k tail is a
+    K-tile (the ring's prologue and clamped restaging only).  Grids of at most
+    64 256-tiles split k (f32 partials, one reduce that rounds once):
+    (2048, 2048, 2112) 4 chunks, (1536, 2312, 704) 2 with ragged edge tiles,
+    (1024, 1024, 8192) 16, (1002, 1032, 4096) 13 with m % 4 != 0 (the partials'
+    scalar stores; TN / TT only, the others take the 128 x 128 kernel).  (k a multiple of 64: a k tail is a
     second pass that adds to the already rounded C.)"""
     m, n, k = shape
     rng = np.random.default_rng(m + n + k)
