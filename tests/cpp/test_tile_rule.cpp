@@ -1,0 +1,50 @@
+// Host-side check of the LDS-DMA kernels' tile choice (kernels.hpp prefer_t64)
+// and split-k plan (dma_plan) on the shapes the round-4 measurements set them
+// by (profiles/r04_t64_rule_ab.log, r04_small_t64_ab.log, r04_t64_waves8_ab.log).
+// Built and run by tests/test_capi_cpu.py (no GPU needed).
+#include <cstdio>
+#include "kernels.hpp"
+
+using elx::kern::i64;
+
+static int bad = 0;
+
+static void expect(bool got, bool want, const char* what, i64 m, i64 n) {
+    if (got != want) {
+        std::printf("FAIL %s m=%lld n=%lld: got %d want %d\n", what, (long long)m, (long long)n, got, want);
+        ++bad;
+    }
+}
+
+int main() {
+    using elx::kern::prefer_t64;
+    struct Case { i64 m, n; bool f32, f64; };
+    const Case cases[] = {
+        {2048, 2048, false, true},   // 256 128-tiles: fp64 takes 64 x 64 (eight waves beat one workgroup per CU)
+        {1536, 2048, true, true},    // 192: fewer than the CUs
+        {2560, 2560, true, true},    // 400: balance 0.78 vs 0.89
+        {3072, 3072, true, true},    // 576: balance 0.56 vs 1.0
+        {3584, 3584, true, true},    // 784
+        {2048, 4096, false, false},  // 512: a multiple of 256
+        {4096, 4096, false, false},  // 1024
+        {1024, 1024, true, true},    // 64
+        {16384, 16384, false, false},
+        {32768, 32768, false, false},
+        {8192, 524288 / 64, false, false},
+    };
+    for (const Case& c : cases) {
+        expect(prefer_t64(1, c.m, c.n), c.f32, "fp32 rule", c.m, c.n);
+        expect(prefer_t64(1, c.m, c.n, 256), c.f64, "fp64 rule", c.m, c.n);
+        expect(prefer_t64(0, c.m, c.n, 256), false, "mode 0", c.m, c.n);
+        expect(prefer_t64(2, c.m, c.n), true, "mode 2", c.m, c.n);
+    }
+    // dma_plan: whole k once the tiles fill two slots per CU; split-k below
+    const elx::kern::DmaPlan big = elx::kern::dma_plan(true, 1024, 4096, 16);
+    if (!big.use || big.nz != 1 || big.kmain != 4096) { std::printf("FAIL plan 1024 tiles\n"); ++bad; }
+    const elx::kern::DmaPlan few = elx::kern::dma_plan(true, 64, 2048, 16);  // 1024^2 in 128-tiles
+    if (!few.use || few.nz != 4 || few.kchunk * few.nz < few.kmain) { std::printf("FAIL plan 64 tiles: nz %d\n", few.nz); ++bad; }
+    const elx::kern::DmaPlan t64 = elx::kern::dma_plan(true, 256, 2048, 16);  // 1024^2 in 64-tiles
+    if (!t64.use || t64.nz != 1) { std::printf("FAIL plan 256 tiles: nz %d\n", t64.nz); ++bad; }
+    std::printf("%s (%d failures)\n", bad ? "FAILED" : "ok", bad);
+    return bad ? 1 : 0;
+}

@@ -148,6 +148,21 @@ def test_cpp_dropin_header_compiles_and_runs(tmp_path):
     assert "OK" in res.stdout
 
 
+def test_lds_dma_tile_rule(tmp_path):
+    """The fp64 / fp32 LDS-DMA kernels' 128 x 128 vs 64 x 64 tile choice and the
+    split-k plan (kernels.hpp prefer_t64, dma_plan) on the shapes the round-4
+    measurements set them by: host-only code, compiled against the HIP headers."""
+    gxx = shutil.which("g++")
+    if gxx is None or not os.path.isdir("/opt/rocm/include"):
+        pytest.skip("no g++ / HIP headers")
+    exe = tmp_path / "test_tile_rule"
+    subprocess.check_call([gxx, "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", "-I", os.path.join(ROOT, "elemental_amd", "csrc", "kernels"),
+                           os.path.join(ROOT, "tests", "cpp", "test_tile_rule.cpp"), "-o", str(exe)])
+    res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0, res.stdout + res.stderr
+
+
 def test_c_header_is_plain_c():
     gcc = shutil.which("gcc")
     if gcc is None:
