@@ -520,16 +520,20 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
     const i64 tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
     // split-k where the tiles leave at least three quarters of the CUs idle:
-    // chunks of >= 4 K-tiles, up to one workgroup per CU; f32 partials in the
+    // chunks of >= 4 K-tiles (16 at 64 tiles), up to one workgroup per CU; f32 partials in the
     // stream-ordered workspace, one reduce that applies alpha / beta and rounds
     // once.  bf16 1024^2 x 8192 41 -> 350 TF, 2048^2 x 8192 481 -> 866, 1024^3 32 ->
-    // 69, 2048^3 326 -> 362; at 2560^2 (100 tiles) three chunks lost 22 % and at
+    // 69, 2048^3 326 -> 381; at 2560^2 (100 tiles) three chunks lost 22 % and at
     // 3072^2 (144) two lost 35 %, so those stay whole (profiles/r04_h16_split_ab.log,
-    // r04_h16_split_ab2.log).  ELX_H16_SPLIT=0 disables.
-    static const bool split_on = [] { const char* v = getenv("ELX_H16_SPLIT"); return !v || v[0] != '0'; }();
+    // r04_h16_split_ab2.log).  ELX_H16_SPLIT = z caps the chunk count (0 or 1: none).
+    static const i64 split_cap = [] { const char* v = getenv("ELX_H16_SPLIT"); return v ? (i64)atoi(v) : (i64)64; }();
     i64 nz = 1, kchunk = kmain;
-    if (split_on && tiles <= 64 && kmain >= 8 * BK) {
-        const i64 z = std::min<i64>((256 + tiles - 1) / tiles, kmain / (4 * BK));
+    if (split_cap > 1 && tiles <= 64 && kmain >= 8 * BK) {
+        // chunks of >= 16 K-tiles at 64 tiles, where the partials' traffic is
+        // m n z words against k / z of MFMAs (2048^3: 2 chunks 381 TF, 4 chunks
+        // 359; 2048^2 x 8192: 4 chunks 857, 2: 756; profiles/r04_h16_split_cap_ab.log)
+        const i64 min_kt = tiles >= 64 ? 16 : 4;
+        const i64 z = std::min<i64>(std::min<i64>((256 + tiles - 1) / tiles, kmain / (min_kt * BK)), split_cap);
         if (z >= 2) {
             kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
             nz = (kmain + kchunk - 1) / kchunk;

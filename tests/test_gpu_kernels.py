@@ -235,7 +235,7 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape):
     wraps of their LDS ring); 2312 columns: ragged edge tiles; k = 64: a single
     K-tile (the ring's prologue and clamped restaging only).  Grids of at most
     64 256-tiles split k (f32 partials, one reduce that rounds once):
-    (2048, 2048, 2112) 4 chunks, (1536, 2312, 704) 2 with ragged edge tiles,
+    (2048, 2048, 2112) 2 chunks, (1536, 2312, 704) 2 with ragged edge tiles,
     (1024, 1024, 8192) 16, (1002, 1032, 4096) 13 with m % 4 != 0 (the partials'
     scalar stores; TN / TT only, the others take the 128 x 128 kernel).  (k a multiple of 64: a k tail is a
     second pass that adds to the already rounded C.)"""
