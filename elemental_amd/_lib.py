@@ -65,6 +65,8 @@ _SIGS = {
     "elx_pool_set_max_cached": (_i, [c_size_t]),
     "elx_pool_max_cached": (_i, [POINTER(c_size_t)]),
     "elx_pool_bin_bytes": (c_size_t, [c_size_t]),
+    "elx_pool_bin_cacheable": (_i, [c_size_t]),
+    "elx_pool_backing_reserved": (_i, [POINTER(c_size_t)]),
     "elx_memcpy_h2d": (_i, [_vp, _vp, c_size_t, _vp]),
     "elx_memcpy_d2h": (_i, [_vp, _vp, c_size_t, _vp]),
     "elx_memcpy_d2d": (_i, [_vp, _vp, c_size_t, _vp]),

@@ -125,6 +125,12 @@ int elx_pool_stats(size_t* reserved, size_t* in_use) { return Guard([&] { Runtim
 int elx_pool_set_max_cached(size_t bytes) { return Guard([&] { Runtime::Get().SetMaxCached(bytes); }); }
 int elx_pool_max_cached(size_t* bytes) { return Guard([&] { *bytes = Runtime::Get().MaxCached(); }); }
 size_t elx_pool_bin_bytes(size_t bytes) { return Runtime::BinBytes(bytes); }
+int elx_pool_bin_cacheable(size_t bytes) {
+    bool c = true;
+    (void)Runtime::BinBytes(bytes, &c);
+    return c ? 1 : 0;
+}
+int elx_pool_backing_reserved(size_t* bytes) { return Guard([&] { *bytes = Runtime::Get().BackingReserved(); }); }
 int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
     return Guard([&] {
         hipStream_t s = S(stream);
@@ -458,12 +464,14 @@ int elx_watchdog_stage(const char* name, double seconds) { return Guard([&] { Wa
 int elx_watchdog_epitaph(const char* text, int exit_code) { return Guard([&] { WatchdogEpitaph(text, exit_code); }); }
 int elx_comm_allgather(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "allgather: negative count ", count);
         const Device d = c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU;
         c->c->AllGather(ToDType(dtype), send, recv, count, d, d == Device::GPU ? S(stream) : nullptr);
     });
 }
 int elx_comm_reduce_scatter(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "reduce_scatter: negative count ", count);
         const Device d = c->c->kind() == Comm::Kind::RCCL ? Device::GPU : Device::CPU;
         c->c->ReduceScatter(ToDType(dtype), send, recv, count, d, d == Device::GPU ? S(stream) : nullptr);
     });
@@ -479,16 +487,22 @@ int elx_comm_split(elx_comm_t c, int color, int key, elx_comm_t* out) {
     return Guard([&] { *out = new elx_comm_s{c->c->Split(color, key)}; });
 }
 int elx_comm_allreduce(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
-    return Guard([&] { c->c->AllReduce(ToDType(dtype), send, recv, count, CommDev(c), CommStream(c, stream)); });
+    return Guard([&] {
+        ELX_REQUIRE(count >= 0, "allreduce: negative count ", count);
+        c->c->AllReduce(ToDType(dtype), send, recv, count, CommDev(c), CommStream(c, stream));
+    });
 }
 int elx_comm_bcast(elx_comm_t c, int dtype, void* buf, int64_t count, int root, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "bcast: negative count ", count);
         ELX_REQUIRE(root >= 0 && root < c->c->Size(), "bcast: root ", root, " outside the communicator");
         c->c->Bcast(ToDType(dtype), buf, count, root, CommDev(c), CommStream(c, stream));
     });
 }
 int elx_comm_alltoall(elx_comm_t c, int dtype, const void* send, void* recv, int64_t count, void* stream) {
-    return Guard([&] {  // El::mpi::AllToAll (AllToAll.hpp:11-105): `count` elements to and from every rank
+    return Guard([&] {
+        // El::mpi::AllToAll (AllToAll.hpp:11-105): `count` elements to and from every rank
+        ELX_REQUIRE(count >= 0, "alltoall: negative count ", count);
         const int p = c->c->Size();
         std::vector<Int> cnt(p, count), dsp(p);
         for (int q = 0; q < p; ++q) dsp[q] = (Int)q * count;
@@ -498,6 +512,7 @@ int elx_comm_alltoall(elx_comm_t c, int dtype, const void* send, void* recv, int
 int elx_comm_sendrecv(elx_comm_t c, int dtype, const void* send, int dest, void* recv, int src, int64_t count,
                       void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "sendrecv: negative count ", count);
         ELX_REQUIRE(dest >= 0 && dest < c->c->Size() && src >= 0 && src < c->c->Size(), "sendrecv: peer outside the communicator");
         c->c->SendRecv(ToDType(dtype), send, dest, recv, src, count, CommDev(c), CommStream(c, stream));
     });
@@ -539,6 +554,7 @@ ReduceOp ToOp(int op) {
 int elx_mpi_allgather(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
                       void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "allgather: negative count ", count);
         const DType t = ToCommDType(dtype);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
         MpiRun(c, device, stream, send, b, recv, b * c->c->Size(), false,
@@ -548,6 +564,7 @@ int elx_mpi_allgather(elx_comm_t c, int dtype, int device, const void* send, voi
 int elx_mpi_reduce_scatter(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv,
                            int64_t count, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "reduce_scatter: negative count ", count);
         const DType t = ToCommDType(dtype);
         const ReduceOp o = ToOp(op);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
@@ -558,6 +575,7 @@ int elx_mpi_reduce_scatter(elx_comm_t c, int dtype, int device, int op, const vo
 int elx_mpi_allreduce(elx_comm_t c, int dtype, int device, int op, const void* send, void* recv, int64_t count,
                       void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "allreduce: negative count ", count);
         const DType t = ToCommDType(dtype);
         const ReduceOp o = ToOp(op);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
@@ -568,6 +586,7 @@ int elx_mpi_allreduce(elx_comm_t c, int dtype, int device, int op, const void* s
 int elx_mpi_alltoall(elx_comm_t c, int dtype, int device, const void* send, void* recv, int64_t count,
                      void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "alltoall: negative count ", count);
         const DType t = ToCommDType(dtype);
         const int p = c->c->Size();
         const size_t b = static_cast<size_t>(count) * DTypeSize(t) * p;
@@ -580,6 +599,7 @@ int elx_mpi_alltoall(elx_comm_t c, int dtype, int device, const void* send, void
 }
 int elx_mpi_bcast(elx_comm_t c, int dtype, int device, void* buf, int64_t count, int root, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(count >= 0, "bcast: negative count ", count);
         ELX_REQUIRE(root >= 0 && root < c->c->Size(), "bcast: root ", root, " outside the communicator");
         const DType t = ToCommDType(dtype);
         const size_t b = static_cast<size_t>(count) * DTypeSize(t);
@@ -590,6 +610,7 @@ int elx_mpi_bcast(elx_comm_t c, int dtype, int device, void* buf, int64_t count,
 int elx_mpi_sendrecv(elx_comm_t c, int dtype, int device, const void* send, int64_t scount, int dest, void* recv,
                      int64_t rcount, int src, void* stream) {
     return Guard([&] {
+        ELX_REQUIRE(scount >= 0 && rcount >= 0, "sendrecv: negative count");
         const DType t = ToCommDType(dtype);
         const size_t es = DTypeSize(t);
         MpiRun(c, device, stream, send, static_cast<size_t>(scount) * es, recv, static_cast<size_t>(rcount) * es,
@@ -675,7 +696,7 @@ int elx_dm_make_uniform(elx_dm_t A, double center, double radius) {
 }
 int elx_dm_synchronize(elx_dm_t A) { return Guard([&] { M(A).Synchronize(); }); }
 int elx_dm_set_stream(elx_dm_t A, void* stream) {
-    return Guard([&] { M(A).SetSyncStream(stream ? static_cast<hipStream_t>(stream) : Runtime::Get().ComputeStream()); });
+    return Guard([&] { M(A).SetStream(stream ? static_cast<hipStream_t>(stream) : Runtime::Get().ComputeStream()); });
 }
 int elx_dm_stream(elx_dm_t A, void** stream) { return Guard([&] { *stream = M(A).Stream(); }); }
 int elx_dm_write(elx_dm_t A, const char* basename, int format, int int_bytes) {

@@ -723,8 +723,8 @@ struct Fd {
 // Handshake: each client sends kRdvMagic, its rank and the world size; rank 0
 // serves each valid rank in 1..size-1 once and drops anything else (a stray
 // connection never uses up a peer's slot, and the id is sent only to peers
-// that name this rendezvous).  Rank 0 binds the address the peers dial
-// (MASTER_ADDR; INADDR_ANY only if that address is not local).
+// that name this rendezvous).  Rank 0 listens on INADDR_ANY; the peers dial
+// MASTER_ADDR.
 namespace {
 constexpr char kRdvMagic[8] = {'E', 'L', 'X', 'R', 'D', 'V', '0', '1'};
 struct RdvHello {
@@ -756,14 +756,13 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
         if (ls.fd < 0) throw CommError("rendezvous: socket() failed");
         const int one = 1;
         ::setsockopt(ls.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0) {
-            if (errno != EADDRNOTAVAIL)
-                throw CommError(Cat("rendezvous: bind to ", addr, ":", port, " failed: ", std::strerror(errno)));
-            sockaddr_in any = sa;  // MASTER_ADDR names another interface (NAT, alias): listen on all
-            any.sin_addr.s_addr = htonl(INADDR_ANY);
-            if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&any), sizeof(any)) != 0)
-                throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
-        }
+        // Listen on every interface: MASTER_ADDR may resolve to a loopback alias
+        // here (Debian hosts map their own name to 127.0.1.1) while the other
+        // nodes reach the real address.  The handshake rejects stray connections.
+        sockaddr_in any = sa;
+        any.sin_addr.s_addr = htonl(INADDR_ANY);
+        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&any), sizeof(any)) != 0)
+            throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
         if (::listen(ls.fd, size) != 0) throw CommError("rendezvous: listen() failed");
         std::vector<bool> served(size, false);
         int left = size - 1;
@@ -803,7 +802,7 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
             RecvAll(s.fd, static_cast<char*>(data), bytes, deadline);
             return;
         }
-        if (Now() > deadline) throw CommError(Cat("rendezvous: could not reach rank 0 at ", addr, ":", port));
+        if (Now() > deadline) throw CommError(Cat("rendezvous: could not reach rank 0 at ", addr ? addr : "127.0.0.1", ":", port));
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
 }

@@ -125,6 +125,13 @@ DistMatrix::DistMatrix(std::shared_ptr<Grid> g, DType t, Dist colDist, Dist rowD
     SetLocalSizes();
 }
 
+DistMatrix::~DistMatrix() {
+    if (dev_ != Device::GPU || !buf_ || !buf_->data()) return;
+    const hipStream_t home = buf_->stream();
+    if (!home || !stream_ || home == stream_) return;
+    try { StreamFence(stream_, home); } catch (...) {}
+}
+
 int DistMatrix::ColStride() const { return G().Stride(cdist_); }
 int DistMatrix::RowStride() const { return G().Stride(rdist_); }
 
@@ -309,15 +316,13 @@ std::shared_ptr<DistMatrix> DistMatrix::ViewOn(const DistMatrix& A, std::shared_
     return V;
 }
 
-void DistMatrix::SetSyncStream(hipStream_t s) {
+void DistMatrix::SetStream(hipStream_t s) {
     if (dev_ != Device::GPU || s == stream_) return;
-    hipEvent_t ev;
-    ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    ELX_CHECK_HIP(hipEventRecord(ev, stream_));
-    ELX_CHECK_HIP(hipStreamWaitEvent(s, ev, 0));
-    ELX_CHECK_HIP(hipEventDestroy(ev));
+    if (buf_ && buf_->data()) {
+        StreamFence(stream_, s);
+        if (!viewing_ && buf_->stream() == stream_) buf_->Rebind(s);
+    }
     stream_ = s;
-    if (buf_ && !viewing_) buf_->Rebind(s);
 }
 
 std::shared_ptr<DistMatrix> DistMatrix::Like(Dist cd, Dist rd) const {

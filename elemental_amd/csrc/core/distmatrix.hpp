@@ -79,6 +79,12 @@ private:
 class DistMatrix {
 public:
     DistMatrix(std::shared_ptr<Grid> g, DType t, Dist colDist, Dist rowDist, Device dev, int root = 0);
+    // A matrix whose stream differs from the one its pool storage is returned
+    // on (a view queued on another stream) orders that stream after its own
+    // work before letting go of the storage, so the free's event covers it.
+    ~DistMatrix();
+    DistMatrix(const DistMatrix&) = delete;
+    DistMatrix& operator=(const DistMatrix&) = delete;
 
     // ---- distribution metadata ----
     const Grid& G() const { return *grid_; }
@@ -116,12 +122,13 @@ public:
     // ---- storage ----
     void* Buffer() const;
     hipStream_t Stream() const { return stream_; }
-    // Rebind the stream work on this matrix is ordered on.  Set it before the
-    // first allocation: storage is returned to the pool on its allocation stream.
-    // internal: temporaries and views that live within one call
-    void SetStream(hipStream_t s) { if (dev_ == Device::GPU) stream_ = s; }
-    // the public SetSyncInfo: ordered after the old stream, buffer rebound
-    void SetSyncStream(hipStream_t s);
+    // Move the matrix to stream s (SetSyncInfo): with allocated storage, s is
+    // first ordered after the old stream's queued work, and pool storage this
+    // matrix owns is returned on s from then on.  (The reference refuses the
+    // move once CUB memory is allocated, Memory/impl.hpp:305-316; here it is
+    // fenced instead.)  A view moves alone: its storage stays with its owner,
+    // and ~DistMatrix orders the owner's stream after the view's work.
+    void SetStream(hipStream_t s);
     size_t ElemSize() const { return DTypeSize(dtype_); }
 
     // ---- realignment / resize (ElementMatrix.cpp:170-370 semantics) ----

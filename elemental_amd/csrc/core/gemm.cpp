@@ -469,6 +469,10 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
 
     struct Slot {
         std::shared_ptr<DistMatrix> a, b;                 // gathered panels (owned temporaries)
+        // the panel's views of A and B on the comm stream: kept until the slot
+        // is refilled, so that the owner-stream fence each one issues when it
+        // goes (~DistMatrix) lands behind work the updates already wait for
+        std::shared_ptr<DistMatrix> va, vb;
         std::shared_ptr<const DistMatrix> ua, ub;         // what the update reads (temporary or view)
         hipEvent_t ready = nullptr, done = nullptr;
         bool pending = false;                             // done recorded, not yet waited by comm
@@ -516,6 +520,10 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         auto Bv = IsN(oB) ? DistMatrix::View(B, k0, k1, 0, B.Width()) : DistMatrix::View(B, 0, B.Height(), k0, k1);
         Av->SetStream(ms);
         Bv->SetStream(ms);
+        s.ua.reset();
+        s.ub.reset();
+        s.va = Av;  // releases panel p-1's views (their fence: see Slot)
+        s.vb = Bv;
         const bool prof = gpu && Prof().on;
         Profiler::Rec rec{};
         const int64_t bytes0 = GlobalCommStats().bytes;
@@ -577,6 +585,8 @@ void SummaC(int oA, int oB, double alpha, const DistMatrix& APre, const DistMatr
         for (auto& s : slot) {
             s.ua.reset();
             s.ub.reset();
+            s.va.reset();
+            s.vb.reset();
             s.a.reset();
             s.b.reset();
             ELX_CHECK_HIP(hipEventDestroy(s.ready));

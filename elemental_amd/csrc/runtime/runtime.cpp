@@ -1,6 +1,7 @@
 #include "runtime.hpp"
 #include "../kernels/kernels.hpp"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <limits>
 #include <vector>
@@ -69,26 +70,25 @@ void Runtime::EnsureGPU() {
     // (ELX_COMM_PRIORITY=0: the compute stream's priority instead; A/B timing)
     const char* pe = getenv("ELX_COMM_PRIORITY");
     ELX_CHECK_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, pe && atoi(pe) == 0 ? lo : hi));
+    ELX_CHECK_HIP(hipStreamCreateWithFlags(&release_, hipStreamNonBlocking));
     // The library's own backing pool: other default-pool users of the process
-    // (RCCL, the caller's hipMallocAsync) never share its blocks, and the
-    // caching policy above it is ours, not the driver's (runtime.hpp).
+    // (RCCL, the caller's hipMallocAsync) never share its blocks, and every
+    // reuse decision is the cache's (runtime.hpp): the driver's reuse policies
+    // are off, and the pool keeps what it is given back (threshold = max;
+    // ELX_POOL_RELEASE_THRESHOLD overrides it for tests) until a trim.
     hipMemPoolProps props{};
     props.allocType = hipMemAllocationTypePinned;
     props.handleTypes = hipMemHandleTypeNone;
     props.location.type = hipMemLocationTypeDevice;
     props.location.id = device_;
     ELX_CHECK_HIP(hipMemPoolCreate(&pool_, &props));
-    // The backing pool keeps what it is given back (threshold = max); memory
-    // returns to the driver only in Trim, after a device synchronize.  With a
-    // release threshold of 0 the driver trims at every synchronize, and the
-    // round-4 GPU suite saw stream-ordered reuse of such a pool hand out blocks
-    // whose previous user had not finished (intermittent wrong GEMM results,
-    // gone with the threshold at max as in rounds 1-3).
     uint64_t thresh = std::numeric_limits<uint64_t>::max();
+    if (const char* e = std::getenv("ELX_POOL_RELEASE_THRESHOLD")) thresh = std::strtoull(e, nullptr, 10);
     ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolAttrReleaseThreshold, &thresh));
-    int on = 1;
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseFollowEventDependencies, &on));
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowOpportunistic, &on));
+    int off = 0;
+    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseFollowEventDependencies, &off));
+    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowOpportunistic, &off));
+    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowInternalDependencies, &off));
     if (!max_cached_set_) {
         // H_CUB_MAX_CACHED_SIZE as the reference reads it (cub.cpp:37-43)
         for (const char* v : {"ELX_POOL_MAX_CACHED", "H_CUB_MAX_CACHED_SIZE"}) {
@@ -98,19 +98,83 @@ void Runtime::EnsureGPU() {
     gpu_ready_ = true;
 }
 
-size_t Runtime::BinBytes(size_t b) {
-    // powers of two up to 1 MiB (CUB bin_growth 2, cub.cpp:21-24), then eight
-    // bins per octave with a 2 MiB floor: ≤ 12.5 % slack on multi-GiB panels
-    if (b <= 512) return 512;
+namespace {
+// The bin geometry (cub.cpp:21-35): ELX's default, or CUB's when any of
+// H_CUB_BIN_GROWTH / H_CUB_MIN_BIN / H_CUB_MAX_BIN is set.
+struct BinConfig {
+    bool cub = false;
+    unsigned growth = 2, min_bin = 1, max_bin = ~0u;  // max_bin ~0u: CUB's INVALID_BIN (no limit)
+    bool debug = false;
+};
+unsigned EnvUint(const char* name, unsigned def, bool& set) {
+    const char* e = std::getenv(name);
+    if (!e || !*e) return def;
+    set = true;
+    return static_cast<unsigned>(std::strtoul(e, nullptr, 10));
+}
+const BinConfig& Bins() {
+    static const BinConfig c = [] {
+        BinConfig b;
+        bool set = false;
+        b.growth = std::max(2u, EnvUint("H_CUB_BIN_GROWTH", 2, set));
+        b.min_bin = EnvUint("H_CUB_MIN_BIN", 1, set);
+        b.max_bin = EnvUint("H_CUB_MAX_BIN", ~0u, set);
+        b.cub = set;
+        bool dset = false;
+        b.debug = EnvUint("H_CUB_DEBUG", 0, dset) != 0;
+        return b;
+    }();
+    return c;
+}
+constexpr size_t kGranule = 512;  // every block is a multiple of 512 B (256-B aligned pointers)
+size_t RoundUp(size_t b, size_t g) { return (b + g - 1) / g * g; }
+constexpr size_t kSizeMax = std::numeric_limits<size_t>::max();
+size_t MulSat(size_t a, unsigned g) { return a > kSizeMax / g ? kSizeMax : a * g; }
+// growth^k, saturating at SIZE_MAX
+size_t PowSat(unsigned g, unsigned k) {
+    size_t r = 1;
+    for (unsigned i = 0; i < k && r != kSizeMax; ++i) r = MulSat(r, g);
+    return r;
+}
+const char* StreamTag(hipStream_t s, hipStream_t compute, hipStream_t comm) {
+    return s == compute ? " (compute)" : s == comm ? " (comm)" : "";
+}
+}  // namespace
+
+size_t Runtime::BinBytes(size_t b, bool* cacheable) {
+    const BinConfig& c = Bins();
+    if (cacheable) *cacheable = true;
+    if (c.cub) {
+        // CachingDeviceAllocator::DeviceAllocate: above max_bin_bytes the block
+        // is sized exactly and not cached; else the nearest growth^k >= bytes,
+        // at least growth^min_bin
+        const size_t maxb = c.max_bin == ~0u ? kSizeMax : PowSat(c.growth, c.max_bin);
+        if (b > maxb) {
+            if (cacheable) *cacheable = false;
+            return RoundUp(std::max<size_t>(b, 1), kGranule);
+        }
+        size_t p = PowSat(c.growth, c.min_bin);
+        while (p < b && p != kSizeMax) p = MulSat(p, c.growth);
+        return RoundUp(std::max<size_t>(p, 1), kGranule);
+    }
+    // powers of two up to 1 MiB (CUB bin_growth 2), then eight bins per octave
+    if (b <= kGranule) return kGranule;
     if (b <= (size_t(1) << 20)) {
-        size_t p = 512;
+        size_t p = kGranule;
         while (p < b) p <<= 1;
         return p;
     }
     size_t top = size_t(1) << 20;
-    while ((top << 1) <= b) top <<= 1;
-    const size_t step = std::max<size_t>(size_t(2) << 20, top / 8);
+    while ((top << 1) <= b && top < (size_t(1) << 62)) top <<= 1;
+    const size_t step = top / 8;
     return (b + step - 1) / step * step;
+}
+
+hipEvent_t Runtime::EventLocked() {
+    hipEvent_t ev = nullptr;
+    if (!spare_events_.empty()) { ev = spare_events_.back(); spare_events_.pop_back(); }
+    else ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return ev;
 }
 
 void* Runtime::Backing(size_t bin, hipStream_t s) {
@@ -133,16 +197,31 @@ void* Runtime::Backing(size_t bin, hipStream_t s) {
     return p;
 }
 
+void Runtime::ReturnLocked(void* p, size_t bin, hipEvent_t ready) {
+    // The block's last use must be complete before the backing pool sees it
+    // (the pool may re-back or hand out a freed block before queued work on it
+    // runs: runtime.hpp).  So: the host waits for the free's event, the block is
+    // freed on the private, idle release stream, and the pool trimmed to what
+    // is still allocated from it, as CUB's synchronous cudaFree returns memory.
+    ELX_CHECK_HIP(hipEventSynchronize(ready));
+    ELX_CHECK_HIP(hipFreeAsync(p, release_));
+    ELX_CHECK_HIP(hipStreamSynchronize(release_));
+    ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
+    spare_events_.push_back(ready);
+    if (Bins().debug)
+        std::fprintf(stderr, "elx_pool[dev %d]: returned block %p (%zu bytes) to the driver (cached %zu, live %zu)\n",
+                     device_, p, bin, cached_, live_bin_);
+}
+
 void Runtime::ReleaseCachedLocked(size_t keep) {
-    // largest blocks first; each goes back to the backing pool on the compute
-    // stream behind its free's event (the freeing stream may be gone by now)
+    // largest blocks first, each back to the driver once its free's event is done
     while (cached_ > keep && !cache_.empty()) {
         auto it = std::prev(cache_.end());
-        ELX_CHECK_HIP(hipStreamWaitEvent(compute_, it->second.ready, 0));
-        ELX_CHECK_HIP(hipFreeAsync(it->second.p, compute_));
-        spare_events_.push_back(it->second.ready);
-        cached_ -= it->first;
+        const size_t bin = it->first;
+        const Cached c = it->second;
+        cached_ -= bin;
         cache_.erase(it);
+        ReturnLocked(c.p, bin, c.ready);
     }
 }
 
@@ -150,13 +229,14 @@ void* Runtime::Alloc(size_t bytes, hipStream_t s) {
     EnsureGPU();
     if (bytes == 0) return nullptr;
     if (!s) s = compute_;
-    const size_t bin = BinBytes(bytes);
+    bool cacheable = true;
+    const size_t bin = BinBytes(bytes, &cacheable);
     std::lock_guard<std::mutex> lk(mu_);
     void* p = nullptr;
     // ELX_POOL_CACHE=0 (debug): no caching, every request from the backing pool
     static const bool nocache = [] { const char* e = std::getenv("ELX_POOL_CACHE"); return e && e[0] == '0'; }();
     auto [lo, hi] = cache_.equal_range(bin);
-    if (nocache) lo = hi;
+    if (nocache || !cacheable) lo = hi;
     if (lo != hi) {
         // prefer a block last used on this stream, then one whose free has
         // completed, then any (ordered behind its free's event)
@@ -167,16 +247,30 @@ void* Runtime::Alloc(size_t bytes, hipStream_t s) {
             for (auto it = lo; it != hi; ++it)
                 if (hipEventQuery(it->second.ready) == hipSuccess) { pick = it; break; }
         if (pick == hi) pick = lo;
-        if (hipEventQuery(pick->second.ready) != hipSuccess)
-            ELX_CHECK_HIP(hipStreamWaitEvent(s, pick->second.ready, 0));
+        const bool cross = pick->second.stream != s;
+        const bool waits = hipEventQuery(pick->second.ready) != hipSuccess;
+        if (waits) ELX_CHECK_HIP(hipStreamWaitEvent(s, pick->second.ready, 0));
         p = pick->second.p;
+        if (Bins().debug)
+            std::fprintf(stderr,
+                         "elx_pool[dev %d]: reused cached block %p (%zu bytes, bin %zu) for stream %p%s "
+                         "(freed on stream %p%s, event %p%s)\n",
+                         device_, p, bytes, bin, (void*)s, StreamTag(s, compute_, comm_), (void*)pick->second.stream,
+                         StreamTag(pick->second.stream, compute_, comm_), (void*)pick->second.ready,
+                         cross ? (waits ? ": cross-stream reuse, the new stream waits on the event"
+                                        : ": cross-stream reuse, event already complete")
+                               : ": same stream");
         spare_events_.push_back(pick->second.ready);
         cached_ -= bin;
         cache_.erase(pick);
     } else {
         p = Backing(bin, s);
+        if (Bins().debug)
+            std::fprintf(stderr, "elx_pool[dev %d]: allocated new block %p (%zu bytes, bin %zu%s) for stream %p%s\n",
+                         device_, p, bytes, bin, cacheable ? "" : ", uncached", (void*)s,
+                         StreamTag(s, compute_, comm_));
     }
-    live_[p] = Live{bytes, bin};
+    live_[p] = Live{bytes, bin, cacheable};
     in_use_ += bytes;
     live_bin_ += bin;
     // ELX_POOL_POISON=1 (debug): every block handed out is filled with 0xFF
@@ -194,19 +288,21 @@ void Runtime::Free(void* p, hipStream_t s) {
     const Live l = it->second;
     if (!s) s = compute_;
     static const bool nocache = [] { const char* e = std::getenv("ELX_POOL_CACHE"); return e && e[0] == '0'; }();
-    if (nocache || cached_ + l.bin > max_cached_) {
-        ELX_CHECK_HIP(hipFreeAsync(p, s));  // over the cap: back to the backing pool
-    } else {
-        hipEvent_t ev = nullptr;
-        if (!spare_events_.empty()) { ev = spare_events_.back(); spare_events_.pop_back(); }
-        else ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ELX_CHECK_HIP(hipEventRecord(ev, s));
-        cache_.emplace(l.bin, Cached{p, s, ev});
-        cached_ += l.bin;
-    }
+    hipEvent_t ev = EventLocked();
+    ELX_CHECK_HIP(hipEventRecord(ev, s));
     in_use_ -= l.requested;
     live_bin_ -= l.bin;
     live_.erase(it);
+    if (nocache || !l.cacheable || cached_ + l.bin > max_cached_) {
+        ReturnLocked(p, l.bin, ev);  // over the cap / uncacheable: back to the driver
+    } else {
+        cache_.emplace(l.bin, Cached{p, s, ev});
+        cached_ += l.bin;
+        if (Bins().debug)
+            std::fprintf(stderr, "elx_pool[dev %d]: returned block %p (%zu bytes) to the cache, stream %p%s, event %p "
+                                 "(cached %zu)\n",
+                         device_, p, l.bin, (void*)s, StreamTag(s, compute_, comm_), (void*)ev, cached_);
+    }
 }
 
 void Runtime::Trim(size_t keep) {
@@ -236,6 +332,14 @@ void Runtime::Stats(size_t& reserved, size_t& in_use) {
     in_use = in_use_;
 }
 
+size_t Runtime::BackingReserved() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!gpu_ready_) return 0;
+    uint64_t v = 0;
+    ELX_CHECK_HIP(hipMemPoolGetAttribute(pool_, hipMemPoolAttrReservedMemCurrent, &v));
+    return static_cast<size_t>(v);
+}
+
 namespace kern {
 hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t s) {
     try {
@@ -256,6 +360,15 @@ hipError_t workspace_free(void* p, hipStream_t s) {
 }
 }  // namespace kern
 
+void StreamFence(hipStream_t from, hipStream_t to) {
+    if (!from || !to || from == to) return;
+    hipEvent_t ev;
+    ELX_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ELX_CHECK_HIP(hipEventRecord(ev, from));
+    ELX_CHECK_HIP(hipStreamWaitEvent(to, ev, 0));
+    ELX_CHECK_HIP(hipEventDestroy(ev));
+}
+
 void Buffer::Reset(Device d, size_t bytes, hipStream_t s) {
     Release();
     dev_ = d;
@@ -264,7 +377,8 @@ void Buffer::Reset(Device d, size_t bytes, hipStream_t s) {
     owned_ = true;
     if (bytes == 0) return;
     if (d == Device::GPU) {
-        ptr_ = Runtime::Get().Alloc(bytes, s);
+        if (!stream_) stream_ = Runtime::Get().ComputeStream();
+        ptr_ = Runtime::Get().Alloc(bytes, stream_);
     } else {
         ptr_ = std::aligned_alloc(64, (bytes + 63) / 64 * 64);
         if (!ptr_) throw RuntimeError(Cat("host allocation of ", bytes, " bytes failed"));

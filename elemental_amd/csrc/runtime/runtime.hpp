@@ -4,9 +4,13 @@
 // include/El/core/Memory/impl.hpp:113-187).
 //
 // Allocator contract (what `elx_pool_*` promise):
-//  * sizes are rounded to bins (powers of two up to 1 MiB, then eight bins per
-//    octave, at least 2 MiB apart: ≤ 12.5 % slack) and a freed block is cached
-//    under its bin; a request is served from a cached block of exactly its bin;
+//  * sizes are rounded to bins and a freed block is cached under its bin; a
+//    request is served from a cached block of exactly its bin.  Default bins:
+//    powers of two from 512 B to 1 MiB (at most 2x slack, as CUB's growth 2),
+//    then eight per octave (<= 12.5 % slack).  H_CUB_BIN_GROWTH / H_CUB_MIN_BIN /
+//    H_CUB_MAX_BIN (src/core/imports/cub.cpp:21-35) switch to CUB's geometric
+//    bins growth^k, k >= min_bin; a request above growth^max_bin gets a block of
+//    its own size (512-B granules) that is never cached;
 //  * reuse is stream-ordered without a host sync: a block freed on stream F and
 //    handed out on stream S makes S wait on the event recorded on F at the free
 //    (CUB's DeviceFree/DeviceAllocate ready-event rule);
@@ -14,15 +18,28 @@
 //    steady-state loop) reserves nothing new after its first pass, whichever
 //    streams it allocates and frees on;
 //  * cached bytes are capped by H_CUB_MAX_CACHED_SIZE / ELX_POOL_MAX_CACHED /
-//    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE):
-//    a free that would exceed the cap returns the block to the backing pool;
-//  * the backing store is the library's own hipMemPool (hipMemPoolCreate,
-//    release threshold max: memory goes back to the driver only in Trim, after
-//    a device synchronize), never the device's default pool shared with other
-//    users of the process; every device scratch of the library (the split-k
-//    partials too, kern::workspace_alloc) comes from this allocator; a failed
-//    backing allocation releases the cache and retries once before reporting
-//    out-of-memory.
+//    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE); a
+//    block that does not fit under the cap, an uncacheable block and, with
+//    ELX_POOL_CACHE=0, every block leaves the allocator: the host waits for its
+//    free's event, gives it back to the backing pool and trims the pool, so
+//    the memory returns to the driver (CUB's synchronous cudaFree);
+//  * the backing store is the library's own hipMemPool (hipMemPoolCreate),
+//    never the device's default pool shared with other users of the process.
+//    It only ever receives IDLE blocks (their last use complete on the host's
+//    view) and decides no reuse itself: its reuse policies are off and its
+//    release threshold is max (ELX_POOL_RELEASE_THRESHOLD overrides, for
+//    tests).  Round 5 measured why (tools/pool_race_probe.hip,
+//    profiles/r05_pool_race_probe.log): on this ROCm a hipFreeAsync'd block whose
+//    earlier work is still queued can be re-backed or handed out before that
+//    work runs (readers saw zero pages or the next owner's data), and with
+//    follow-event-dependencies on, a stream that once waited on an OLDER event
+//    of the freeing stream receives the block at once.  Every device scratch of
+//    the library (the split-k partials too, kern::workspace_alloc) comes from
+//    this allocator; a failed backing allocation releases the cache and retries
+//    once before reporting out-of-memory;
+//  * H_CUB_DEBUG=1 (cub.cpp:45-50) logs every allocation, reuse (with the
+//    stream it was freed on and the event the new stream waits on), cache
+//    return and release to stderr.
 #pragma once
 #include "../common.hpp"
 #include <map>
@@ -54,21 +71,30 @@ public:
     void Trim(size_t keep);
     // reserved = live + cached bin bytes; in_use = requested bytes still live
     void Stats(size_t& reserved, size_t& in_use);
+    // what the backing hipMemPool itself holds from the driver
+    // (hipMemPoolAttrReservedMemCurrent; 0 before the first GPU use)
+    size_t BackingReserved();
     void SetMaxCached(size_t bytes);
     size_t MaxCached();
-    static size_t BinBytes(size_t bytes);
+    // the bin a request of `bytes` is served from; `cacheable` = false for
+    // requests above H_CUB_MAX_BIN's bin (own-size blocks, never cached)
+    static size_t BinBytes(size_t bytes, bool* cacheable = nullptr);
 
 private:
     struct Cached { void* p; hipStream_t stream; hipEvent_t ready; };
-    struct Live { size_t requested, bin; };
+    struct Live { size_t requested, bin; bool cacheable; };
     Runtime() = default;
     void* Backing(size_t bin, hipStream_t s);
     void ReleaseCachedLocked(size_t keep);
+    // give an idle-to-be block back to the backing pool: the host waits for
+    // `ready`, frees it on the private release stream and trims the pool
+    void ReturnLocked(void* p, size_t bin, hipEvent_t ready);
+    hipEvent_t EventLocked();
     std::mutex mu_;
     bool gpu_ready_ = false;
     int device_ = -1;
     int reserved_cus_ = 0;
-    hipStream_t compute_ = nullptr, comm_ = nullptr;
+    hipStream_t compute_ = nullptr, comm_ = nullptr, release_ = nullptr;
     hipMemPool_t pool_ = nullptr;
     std::unordered_map<void*, Live> live_;
     std::multimap<size_t, Cached> cache_;  // bin bytes -> freed block
@@ -77,6 +103,9 @@ private:
     size_t max_cached_ = ~size_t(0);
     bool max_cached_set_ = false;
 };
+
+// Stream `to` waits for the work queued on `from` so far (no-op when equal or null).
+void StreamFence(hipStream_t from, hipStream_t to);
 
 // RAII device or host buffer.  GPU memory comes from the pool on `stream` and is
 // returned to it on that stream (stream-ordered reuse, no device sync).
@@ -103,6 +132,9 @@ public:
     // release on `s` from now on (the caller has ordered s after the old stream)
     void Rebind(hipStream_t s) { stream_ = s; }
     void* data() const { return ptr_; }
+    // the stream the block is returned to the pool on (GPU blocks we own;
+    // nullptr for host memory and wrapped caller storage)
+    hipStream_t stream() const { return owned_ && dev_ == Device::GPU ? stream_ : nullptr; }
     size_t bytes() const { return bytes_; }
     Device device() const { return dev_; }
 

@@ -539,3 +539,10 @@ def pool_stats() -> tuple[int, int]:
     r, u = c_size_t(), c_size_t()
     call("elx_pool_stats", byref(r), byref(u))
     return r.value, u.value
+
+
+def pool_backing_reserved() -> int:
+    """Bytes the allocator's backing hipMemPool holds from the driver."""
+    r = c_size_t()
+    call("elx_pool_backing_reserved", byref(r))
+    return r.value

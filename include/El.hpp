@@ -455,7 +455,9 @@ void SendRecv(T* buf, int count, int to, int from, Comm const& comm, SyncInfo<D>
     }
     void* tmp = nullptr;
     detail::Check(elx_pool_alloc(&tmp, sizeof(T) * count, detail_::StreamOf(si)));
-    int rc = elx_matrix_copy(dt, ELX_DEVICE_GPU, count, 1, buf, count, tmp, count, detail_::StreamOf(si));
+    // a byte copy: any communication type (Int, int, byte as well as the
+    // matrix types), stream-ordered before the exchange
+    int rc = elx_memcpy_d2d(tmp, buf, sizeof(T) * static_cast<size_t>(count), detail_::StreamOf(si));
     if (rc == ELX_OK)
         rc = elx_mpi_sendrecv(comm.Handle(), dt, ELX_DEVICE_GPU, tmp, count, to, buf, count, from, detail_::StreamOf(si));
     const std::string err = rc == ELX_OK ? std::string() : std::string(elx_last_error());

@@ -141,8 +141,17 @@ int elx_pool_stats(size_t* bytes_reserved, size_t* bytes_in_use);
  * SIZE_MAX = unbounded, the default); lowering it releases cached blocks */
 int elx_pool_set_max_cached(size_t bytes);
 int elx_pool_max_cached(size_t* bytes);
-/* the bin a request of `bytes` is served from (reserved bytes per block) */
+/* the bin a request of `bytes` is served from (reserved bytes per block);
+ * H_CUB_BIN_GROWTH / H_CUB_MIN_BIN / H_CUB_MAX_BIN select CUB's geometric bins
+ * (cub.cpp:21-35, read once per process) */
 size_t elx_pool_bin_bytes(size_t bytes);
+/* 1 when a request of `bytes` is cached on free, 0 when it is above
+ * H_CUB_MAX_BIN's bin (an own-size block returned to the driver on free) */
+int elx_pool_bin_cacheable(size_t bytes);
+/* bytes the backing hipMemPool holds from the driver
+ * (hipMemPoolAttrReservedMemCurrent): live + cached blocks once blocks that
+ * left the cache were trimmed back */
+int elx_pool_backing_reserved(size_t* bytes);
 int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int elx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int elx_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);

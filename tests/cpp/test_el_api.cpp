@@ -377,6 +377,17 @@ int main() {
         for (int i = 0; i < n; ++i) EXPECT(T.Get(i, 0) == 10.0 * ((me + p - 1) % p) + i - 2.0);
         El::mpi::SendRecv(B.Buffer(), n, (me + 1) % p, (me + p - 1) % p, comm, si);  // in place
         for (int i = 0; i < n; ++i) EXPECT(B.Get(i, 0) == 7.0 + i);
+        {  // in-place SendRecv of Int and byte buffers on the test's device
+            El::Matrix<El::Int, kDev> I(3, 1);
+            El::Matrix<unsigned char, kDev> U(5, 1);
+            for (int i = 0; i < 3; ++i) I.Set(i, 0, 100 * me + i);
+            for (int i = 0; i < 5; ++i) U.Set(i, 0, static_cast<unsigned char>(10 * me + i));
+            El::mpi::SendRecv(I.Buffer(), 3, (me + 1) % p, (me + p - 1) % p, comm, El::SyncInfoFromMatrix(I));
+            El::mpi::SendRecv(U.Buffer(), 5, (me + 1) % p, (me + p - 1) % p, comm, El::SyncInfoFromMatrix(U));
+            const int src = (me + p - 1) % p;
+            for (int i = 0; i < 3; ++i) EXPECT(I.Get(i, 0) == 100 * src + i);
+            for (int i = 0; i < 5; ++i) EXPECT(U.Get(i, 0) == static_cast<unsigned char>(10 * src + i));
+        }
         double scalar = me == 0 ? 4.25 : 0.0;
         El::mpi::Broadcast(scalar, 0, comm, El::SyncInfo<El::Device::CPU>{});
         EXPECT(scalar == 4.25);

@@ -75,15 +75,16 @@ def test_gpu_matrix_without_device_fails_loudly():
 
 def test_pool_bins_and_cap_setting_without_device():
     """The caching allocator's bin rule (powers of two to 1 MiB, then eight bins
-    per octave with a 2 MiB floor: runtime.hpp's contract) and its cap setting
+    per octave: runtime.hpp's contract) and its cap setting
     (H_CUB_MAX_CACHED_SIZE, cub.cpp:37-43) need no device."""
     lib = L.lib()
     assert [lib.elx_pool_bin_bytes(b) for b in (0, 1, 512, 513, 5000, 1 << 20)] == [512, 512, 512, 1024, 8192, 1 << 20]
-    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == 2 << 20
+    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == (1 << 20) + (128 << 10)
     prev = 0
-    for b in [(3 << 20) + 7, 100 << 20, (1 << 30) + 1, 5 << 30, 32 << 30, (1 << 35) + 3]:
+    for b in [(1 << 20) + 1, (3 << 20) + 7, 100 << 20, (1 << 30) + 1, 5 << 30, 32 << 30, (1 << 35) + 3]:
         bb = lib.elx_pool_bin_bytes(b)
-        assert b <= bb <= b * 1.125 + (2 << 20) and bb % (2 << 20) == 0 and bb > prev
+        assert b <= bb <= b * 1.125 and bb % (128 << 10) == 0 and bb > prev
+        assert lib.elx_pool_bin_cacheable(b) == 1
         prev = bb
     old = L.ctypes.c_size_t()
     L.call("elx_pool_max_cached", L.ctypes.byref(old))
@@ -94,6 +95,55 @@ def test_pool_bins_and_cap_setting_without_device():
         assert v.value == 123 << 20
     finally:
         L.call("elx_pool_set_max_cached", old.value)
+    r = L.ctypes.c_size_t(7)
+    L.call("elx_pool_backing_reserved", L.ctypes.byref(r))
+    assert r.value == 0  # no device touched: no backing pool yet
+
+
+def _cub_bin(b, growth, min_bin, max_bin):
+    """hipCUB CachingDeviceAllocator::DeviceAllocate's bin choice (the
+    reference's pool, configured by cub.cpp:21-35): above growth^max_bin the
+    request is its own (uncached) block; else the smallest growth^k >= bytes,
+    at least growth^min_bin.  Blocks here are whole 512-B granules."""
+    gran = lambda x: max(512, (x + 511) // 512 * 512)  # noqa: E731
+    if max_bin is not None and b > growth ** max_bin:
+        return gran(b), 0
+    p = growth ** min_bin
+    while p < b:
+        p *= growth
+    return gran(p), 1
+
+
+@pytest.mark.parametrize("env", [
+    {"H_CUB_BIN_GROWTH": "2"},
+    {"H_CUB_BIN_GROWTH": "8"},
+    {"H_CUB_BIN_GROWTH": "3", "H_CUB_MIN_BIN": "7"},
+    {"H_CUB_MIN_BIN": "12"},
+    {"H_CUB_MAX_BIN": "20"},
+    {"H_CUB_BIN_GROWTH": "4", "H_CUB_MIN_BIN": "3", "H_CUB_MAX_BIN": "12"},
+])
+def test_pool_cub_bin_knobs(env):
+    """H_CUB_BIN_GROWTH / H_CUB_MIN_BIN / H_CUB_MAX_BIN (cub.cpp:21-35) switch
+    the bins to CUB's geometric ones; sizes above the max bin are own-size,
+    uncached blocks.  Read once per process, so each setting runs in its own."""
+    import json
+    import os
+    import subprocess
+    import sys
+    sizes = [0, 1, 100, 511, 512, 513, 4096, 5000, 65537, 1 << 20, (1 << 20) + 1, 3 << 20, 123456789, 5 << 30]
+    code = ("import json,sys; sys.path.insert(0, %r); from elemental_amd import _lib as L; lib = L.lib(); "
+            "print(json.dumps([[lib.elx_pool_bin_bytes(b), lib.elx_pool_bin_cacheable(b)] for b in %r]))"
+            % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), sizes))
+    e = {k: v for k, v in os.environ.items() if not k.startswith("H_CUB_")}
+    e.update(env)
+    out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    g = int(env.get("H_CUB_BIN_GROWTH", 2))
+    mn = int(env.get("H_CUB_MIN_BIN", 1))
+    mx = int(env["H_CUB_MAX_BIN"]) if "H_CUB_MAX_BIN" in env else None
+    want = [list(_cub_bin(b, g, mn, mx)) for b in sizes]
+    assert got == want, list(zip(sizes, got, want))
 
 
 def test_cpu_matrices_local_gemm_and_redistribution():
@@ -248,3 +298,29 @@ def test_gemm_suite_driver_cpu(tmp_path):
                                                       "41", "8"]
     assert len(lines) == 5 and all(len(ln.split(":")) == 12 for ln in lines)
     assert lines[2].startswith("CPU:float:Normal:Transpose:SUMMA_B:")
+
+
+def test_mpi_collectives_reject_negative_counts():
+    """Every El::mpi / raw collective entry checks count >= 0 before it sizes a
+    buffer or hands the count to RCCL (a negative int64 would become a huge
+    size_t there)."""
+    c = el.Comm.self_comm()
+    buf = np.zeros(8)
+    p = buf.ctypes.data
+    CPU = L.CPU
+    calls = [
+        ("elx_mpi_allgather", (c.h, L.F64, CPU, p, p, -1, None)),
+        ("elx_mpi_reduce_scatter", (c.h, L.F64, CPU, 0, p, p, -2, None)),
+        ("elx_mpi_allreduce", (c.h, L.F64, CPU, 0, p, p, -1, None)),
+        ("elx_mpi_alltoall", (c.h, L.F64, CPU, p, p, -3, None)),
+        ("elx_mpi_bcast", (c.h, L.F64, CPU, p, -1, 0, None)),
+        ("elx_mpi_sendrecv", (c.h, L.F64, CPU, p, -1, 0, p, 1, 0, None)),
+        ("elx_mpi_sendrecv", (c.h, L.F64, CPU, p, 1, 0, p, -1, 0, None)),
+        ("elx_comm_allgather", (c.h, L.F64, p, p, -1, None)),
+        ("elx_comm_allreduce", (c.h, L.F64, p, p, -1, None)),
+        ("elx_comm_bcast", (c.h, L.F64, p, -1, 0, None)),
+    ]
+    for name, args in calls:
+        with pytest.raises(L.LogicError, match="negative count"):
+            L.call(name, *args)
+    assert np.all(buf == 0)

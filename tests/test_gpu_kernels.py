@@ -572,18 +572,20 @@ def test_pool_alloc_free():
 
 
 def test_pool_bins_and_cap():
-    """Bins (powers of two to 1 MiB, then 8 per octave, >= 2 MiB apart) and the
+    """Bins (powers of two to 1 MiB, then 8 per octave) and the
     H_CUB_MAX_CACHED_SIZE cap (cub.cpp:37-43): a free past the cap returns the
-    block instead of caching it, so reserved - in_use never exceeds the cap."""
+    block to the driver instead of caching it (CUB's cudaFree), so
+    reserved - in_use never exceeds the cap, and the backing pool's own
+    reservation (hipMemPoolAttrReservedMemCurrent) drops with it."""
     lib = L.lib()
     assert lib.elx_pool_bin_bytes(1) == 512
     assert lib.elx_pool_bin_bytes(5000) == 8192
     assert lib.elx_pool_bin_bytes(1 << 20) == 1 << 20
-    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == 2 << 20
-    assert lib.elx_pool_bin_bytes(3 << 20) == 4 << 20
-    for b in [(1 << 30) + 1, 5 << 30, (1 << 33) + 12345, 32 << 30]:
+    assert lib.elx_pool_bin_bytes((1 << 20) + 1) == (1 << 20) + (128 << 10)
+    assert lib.elx_pool_bin_bytes(3 << 20) == 3 << 20
+    for b in [(1 << 20) + 1, 5 << 20, (1 << 30) + 1, 5 << 30, (1 << 33) + 12345, 32 << 30]:
         bb = lib.elx_pool_bin_bytes(b)
-        assert b <= bb <= b * 1.125 + (2 << 20)
+        assert b <= bb <= b * 1.125
     el.device_synchronize()
     old = ctypes.c_size_t()
     L.call("elx_pool_max_cached", ctypes.byref(old))
@@ -592,18 +594,64 @@ def test_pool_bins_and_cap():
         L.call("elx_pool_set_max_cached", cap)
         r, u = el.pool_stats()
         assert r - u <= cap
+        base = el.pool_backing_reserved()
         ptrs = []
         for _ in range(6):
             p = ctypes.c_void_p()
             L.call("elx_pool_alloc", ctypes.byref(p), 3 << 20, None)
             ptrs.append(p)
+        held = el.pool_backing_reserved()
+        assert held >= base + 6 * (3 << 20) - cap, (base, held)
         for p in ptrs:
             L.call("elx_pool_free", p, None)
         r, u = el.pool_stats()
         assert r - u <= cap, (r, u)
+        # what left the cache left the process: the backing pool holds the live
+        # and cached blocks only
+        assert el.pool_backing_reserved() <= r + (2 << 20), (el.pool_backing_reserved(), r, u)
     finally:
         L.call("elx_pool_set_max_cached", old.value)
         el.device_synchronize()
+
+
+def _pool_worker(case, **env):
+    import os
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    e.update(env)
+    here = os.path.dirname(os.path.abspath(__file__))
+    return subprocess.run([sys.executable, os.path.join(here, "_pool_workers.py"), case], env=e,
+                          capture_output=True, text=True, timeout=120)
+
+
+@pytest.mark.parametrize("cache", ["1", "0"])
+def test_pool_threshold0_delayed_reader(cache):
+    """Round 4's wrong GEMMs, as one deterministic regression test: the backing
+    pool's release threshold at 0 (ELX_POOL_RELEASE_THRESHOLD=0: the driver
+    trims at every synchronize), a reader delayed ~0.2 s by a spin kernel on its
+    own stream, the block freed behind it (pool level, and a DistMatrix view on
+    another stream dropped before its owner), and the same bin requested and
+    overwritten at once on another stream.  With and without the cache
+    (ELX_POOL_CACHE=0 sends every free to the driver)."""
+    cases = ["pool_free_after_delayed_reader", "view_on_other_stream", "set_stream_owned"]
+    for c in cases:
+        r = _pool_worker(c, ELX_POOL_RELEASE_THRESHOLD="0", ELX_POOL_CACHE=cache)
+        assert r.returncode == 0 and f"OK {c}" in r.stdout, (c, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_pool_debug_trace_lists_cross_stream_reuse():
+    """H_CUB_DEBUG=1 (cub.cpp:45-50): the trace names each allocation, cache
+    return and reuse with its streams and event; a block freed on one stream
+    while its work still runs and requested on another is reported as a
+    cross-stream reuse that makes the new stream wait on the free's event."""
+    r = _pool_worker("debug_trace_cross_stream", H_CUB_DEBUG="1")
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [x for x in r.stderr.splitlines() if x.startswith("elx_pool[")]
+    assert any("allocated new block" in x for x in lines), lines
+    assert any("to the cache" in x for x in lines), lines
+    reuse = [x for x in lines if "reused cached block" in x]
+    assert reuse and "cross-stream reuse, the new stream waits on the event" in reuse[-1], lines
 
 
 @pytest.mark.parametrize("s", [L.F64, L.F32, L.F16, L.BF16])

@@ -1,12 +1,23 @@
 #!/bin/bash
-# gemm_suite repeated under the allocator's debug knobs (round-4 residual hunt:
-# intermittent wrong results on the second warm-up with threshold-0 pools)
+# gemm_suite repeated with the backing pool's release threshold at 0
+# (ELX_POOL_RELEASE_THRESHOLD=0) and under the allocator's debug knobs: the
+# round-4 wrong-result hunt (intermittent associativity residuals 0.05-5 on the
+# second warm-up with threshold-0 pools).  Usage: tools/pool_debug.sh [reps]
 S=tests/cpp/_build/gemm_suite
-for v in "" "ELX_POOL_POISON=1" "ELX_POOL_CACHE=0"; do
-  for rep in 1 2 3; do
+REPS=${1:-3}
+fails=0
+for v in "ELX_POOL_RELEASE_THRESHOLD=0" "ELX_POOL_RELEASE_THRESHOLD=0 ELX_POOL_CACHE=0" \
+         "ELX_POOL_RELEASE_THRESHOLD=0 ELX_POOL_POISON=1"; do
+  for rep in $(seq 1 "$REPS"); do
     for f in tools/suite_pool_exp.txt tools/suite_pool_exp2.txt; do
       echo "=== env [$v] rep $rep exp $f"
-      env $v timeout -k 5 60 $S --f $f --o /tmp/res.txt --warmup 3 --runs 1 --check 2>&1 | grep -E "residual" || echo "ok"
+      out=$(env $v timeout -k 5 60 $S --f $f --o /tmp/res.txt --warmup 3 --runs 1 --check 2>&1)
+      rc=$?
+      echo "$out" | grep -E "Testing|residual|error" || true
+      echo "rc=$rc"
+      if [ $rc -ge 124 ]; then echo "timeout/abort: stopping"; exit $rc; fi
+      [ $rc -ne 0 ] && fails=$((fails + 1))
     done
   done
 done
+echo "failing runs: $fails"
