@@ -49,8 +49,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int HALF = 128 * BK * 2;  // one half image: 128 rows x 64 k x 2 B = 16 KiB
+constexpr int BK = 64;
+constexpr int HALF = 128 * BK * 2;  // one RC half image: 64 k-rows x 128 operand rows x 2 B = 16 KiB
 
 struct H2Params {
     i64 m, n, k;  // k: multiple of BK
@@ -158,17 +158,18 @@ __device__ __forceinline__ void epi_one(const H2Params& p, const f32x4 v4, i64 i
 
 // every tile with compile-time indices (a fold, not a loop: a loop the unroller
 // declines would index the accumulators dynamically and push them to scratch)
-template <bool BF16, int NI, int... Q>
-__device__ __forceinline__ void epilogue_seq(const H2Params& p, const f32x4 (&acc)[8][NI], i64 rb, i64 cb,
+template <bool BF16, int MI, int NI, int... Q>
+__device__ __forceinline__ void epilogue_seq(const H2Params& p, const f32x4 (&acc)[MI][NI], i64 rb, i64 cb,
                                              std::integer_sequence<int, Q...>) {
     (epi_one<BF16>(p, acc[Q / NI][Q % NI], rb + (Q / NI) * 16, cb + (Q % NI) * 16), ...);
 }
 
-template <bool BF16, int NI>
-__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8][NI], i64 m0, i64 n0, int wr, int wc,
+// wave (wr, wc) owns rows m0 + wr * 16 MI .. and columns n0 + wc * 16 NI ..
+template <bool BF16, int MI, int NI>
+__device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[MI][NI], i64 m0, i64 n0, int wr, int wc,
                                          int l) {
-    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * (16 * NI) + (l & 15);
-    epilogue_seq<BF16, NI>(p, acc, rb, cb, std::make_integer_sequence<int, 8 * NI>{});
+    const i64 rb = m0 + wr * (16 * MI) + 4 * (l >> 4), cb = n0 + wc * (16 * NI) + (l & 15);
+    epilogue_seq<BF16, MI, NI>(p, acc, rb, cb, std::make_integer_sequence<int, MI * NI>{});
 }
 
 // Four-wave kernel: a 256 x 256 output tile over 4 waves (2 x 2), one per
@@ -181,12 +182,18 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
 // MFMAs.  hipBLASLt's bf16 kernels on these shapes have the same geometry
 // (MT256x256x64, MI16x16, 4 waves: profiles/r03_vendor_pmc.json).
 //
-// Staging unit = one operand's K-tile image (256 rows x 64 k = 32 KiB, the KC /
-// RC images: two 128-row halves of 128-B KC rows or 256-B RC k-rows), in a
-// ring of 5 slots (160 KiB): A_t is unit 2t, B_t unit 2t+1, unit u in slot u % 5.
-// Each K-tile runs as two k-steps of 64 MFMAs per wave:
+// The same loop at half the tile (WM = 4: 128 x 128 per workgroup, 64 x 64 =
+// 4 x 4 accumulators per wave, 80 KiB of ring, two workgroups per CU) serves the
+// grids on which 256 x 256 tiles leave CUs idle (fewer than 256 of them: 2048^3
+// has 64, i.e. a quarter of the chip).  Round 5.
+//
+// Staging unit = one operand's K-tile image (BM rows x 64 k: 32 KiB at WM = 8,
+// 16 KiB at WM = 4; the KC / RC images: 128-B KC rows, or 256-B RC k-rows in
+// 128-row halves), in a ring of 5 slots: A_t is unit 2t, B_t unit 2t+1, unit u
+// in slot u % 5.  A unit is 4 WM one-KiB pieces, WM per wave.  Each K-tile runs
+// as two k-steps of WM^2 MFMAs per wave:
 //   (t,0): MFMAs on fragments (t,0) [set X]; read fragments (t,1) [set Y] from
-//          A_t, B_t; stage A_{t+2} into B_{t-1}'s slot; then vmcnt(8) (A_{t+1}
+//          A_t, B_t; stage A_{t+2} into B_{t-1}'s slot; then vmcnt(WM) (A_{t+1}
 //          and B_{t+1} landed, A_{t+2} may stay in flight), lgkmcnt(0), barrier;
 //   (t,1): MFMAs on (t,1) [Y]; read (t+1,0) [X] from A_{t+1}, B_{t+1}; stage
 //          B_{t+2} into A_t's slot; lgkmcnt(0), no barrier.
@@ -196,16 +203,20 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[8
 // No wave can be two k-steps ahead of another (it would have passed a barrier
 // the other has not reached), so one barrier per K-tile suffices.  Units past
 // the end re-stage the last K-tile into a slot nobody reads again, so every
-// k-step issues the same 8 pieces and the counted wait is exact without branches.
+// k-step issues the same WM pieces and the counted wait is exact without branches.
 // The accumulators are tied to AGPRs through inline asm (mfma_acc).
 // ---------------------------------------------------------------------------
 namespace w4 {
-constexpr int UNIT = 256 * BK * 2;  // one operand's K-tile image: 32 KiB
 constexpr int NSLOT = 5;
+template <int WM> struct Geo {
+    static constexpr int BM = 32 * WM;           // tile edge (rows of op(A), columns of op(B))
+    static constexpr int UNIT = BM * BK * 2;     // one operand's K-tile image
+    static constexpr int WROWS = 16 * WM;        // operand rows one wave reads
+};
 
-// per-lane offset (elements from the image's corner at k0) of piece j (0..31)
-// of one operand's K-tile image: half j >> 4, wave-instruction j & 15 of it, as
-// the image is laid out: 16 wave-instructions of 1 KiB per 128-row half
+// per-lane offset (elements from the image's corner at k0) of piece j of one
+// operand's K-tile image, as the image is laid out: KC rows 8j..8j+7 (128 B
+// each), RC k-rows 4(j & 15)..+3 of the 128-row half j >> 4
 template <bool KC>
 __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld) {
     const int h = j >> 4, ins = j & 15;
@@ -229,11 +240,11 @@ __device__ __forceinline__ const uint16_t* tile_base(const uint16_t* X, i64 ld, 
     return KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
 }
 
-template <bool BUF, bool KC>
+template <int BMR, bool BUF, bool KC>
 __device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int j,
                                       lds_char* img) {
     if constexpr (BUF) {
-        const BufferSrc<uint16_t> src(tile_base<KC>(X, ld, R0, k0), (KC ? 256 : BK) * ld * 2);
+        const BufferSrc<uint16_t> src(tile_base<KC>(X, ld, R0, k0), (KC ? BMR : BK) * ld * 2);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + j * 1024), 16,
                                                  off, 0, 0, 0);
     } else {
@@ -241,8 +252,19 @@ __device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0,
     }
 }
 
+// a wave's operand fragment f (16 rows) of k-step s: KC images are one block of
+// 128-B rows; RC images are 128-row halves, so a wave's rows may start inside one
+template <int WM, bool KC>
+__device__ __forceinline__ u32x4 wfrag(const lds_char* img, int w_r, int f, int s, int l) {
+    constexpr int WR = Geo<WM>::WROWS;
+    const int r0 = w_r * WR + f * 16;
+    if constexpr (KC) return frag<true>(img, r0, s, l);
+    else return frag<false>(img + (r0 >> 7) * HALF, r0 & 127, s, l);
+}
+
+template <int WM>
 struct Sets {
-    u32x4 a[8], b[8];
+    u32x4 a[WM], b[WM];
 };
 
 // acc += a b with the accumulator tied to one AGPR quad.  Written as asm: the
@@ -258,23 +280,25 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const u32x4& a, const u32x4
 
 // 8-pass MFMA result -> any non-MFMA reader: 12 wait states (then the registers
 // are handed to the compiler through empty asm statements ordered after the pad)
-__device__ __forceinline__ void settle(f32x4 (&acc)[8][8]) {
+template <int WM>
+__device__ __forceinline__ void settle(f32x4 (&acc)[WM][WM]) {
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) asm volatile("" : "+a"(acc[a][b]));
+        for (int b = 0; b < WM; ++b) asm volatile("" : "+a"(acc[a][b]));
 }
 
 // Split-k partial of one wave: the raw f32 accumulators into W (ld m)
-__device__ __forceinline__ void epilogue_partial(const H2Params& p, const f32x4 (&acc)[8][8], i64 m0, i64 n0, int wr,
-                                                 int wc, int l) {
-    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 128 + (l & 15);
+template <int WM>
+__device__ __forceinline__ void epilogue_partial(const H2Params& p, const f32x4 (&acc)[WM][WM], i64 m0, i64 n0,
+                                                 int wr, int wc, int l) {
+    const i64 rb = m0 + wr * (16 * WM) + 4 * (l >> 4), cb = n0 + wc * (16 * WM) + (l & 15);
     const bool vec = (p.m & 3) == 0;
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
+        for (int ni = 0; ni < WM; ++ni) {
             const i64 i = rb + mi * 16, j = cb + ni * 16;
             if (j >= p.n || i >= p.m) continue;
             float* o = p.W + i + j * p.m;
@@ -305,26 +329,27 @@ __global__ __launch_bounds__(256) void h16_splitk_reduce(i64 m, i64 n, int nz, f
     }
 }
 
-// C tile of one wave (128 x 128): accumulator (mi, ni) holds rows
+// C tile of one wave (16 WM x 16 WM): accumulator (mi, ni) holds rows
 // rb + 16 mi + 4 (l >> 4) + {0..3}, column cb + 16 ni + (l & 15).  One row of
-// accumulators at a time (C loads, then stores), so at most 32 values live in
+// accumulators at a time (C loads, then stores), so at most 4 WM values live in
 // VGPRs; interior tiles with an 8-B-aligned C take the unchecked path.
-template <bool BF16>
-__device__ __forceinline__ void epilogue4(const H2Params& p, const f32x4 (&acc)[8][8], i64 m0, i64 n0, int wr, int wc,
-                                          int l) {
+template <bool BF16, int WM>
+__device__ __forceinline__ void epilogue4(const H2Params& p, const f32x4 (&acc)[WM][WM], i64 m0, i64 n0, int wr,
+                                          int wc, int l) {
     using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
-    const i64 rb = m0 + wr * 128 + 4 * (l >> 4), cb = n0 + wc * 128 + (l & 15);
-    const bool fast = p.vec_c && m0 + BM <= p.m && n0 + BN <= p.n;
+    constexpr int BM = Geo<WM>::BM;
+    const i64 rb = m0 + wr * (16 * WM) + 4 * (l >> 4), cb = n0 + wc * (16 * WM) + (l & 15);
+    const bool fast = p.vec_c && m0 + BM <= p.m && n0 + BM <= p.n;
     if (fast) {
         uint16_t* o0 = p.C + rb + cb * p.ldc;
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-            uint2 cv[8];
+        for (int mi = 0; mi < WM; ++mi) {
+            uint2 cv[WM];
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni)
+            for (int ni = 0; ni < WM; ++ni)
                 cv[ni] = p.beta != 0.f ? *reinterpret_cast<const uint2*>(o0 + mi * 16 + ni * 16 * p.ldc) : make_uint2(0, 0);
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni) {
+            for (int ni = 0; ni < WM; ++ni) {
                 const uint16_t in[4] = {(uint16_t)(cv[ni].x & 0xffff), (uint16_t)(cv[ni].x >> 16),
                                         (uint16_t)(cv[ni].y & 0xffff), (uint16_t)(cv[ni].y >> 16)};
                 uint16_t r16[4];
@@ -339,58 +364,58 @@ __device__ __forceinline__ void epilogue4(const H2Params& p, const f32x4 (&acc)[
             }
         }
     } else {
-        epilogue<BF16, 8>(p, acc, m0, n0, wr, wc, l);
+        epilogue<BF16, WM, WM>(p, acc, m0, n0, wr, wc, l);
     }
 }
 
-struct Pieces {  // this wave's staging pieces w + 4u, u = 0..7, of each operand's image
-    int offA[8], offB[8];
-    i64 gA[8], gB[8];
+template <int WM>
+struct Pieces {  // this wave's staging pieces w + 4u, u = 0..WM-1, of each operand's image
+    int offA[WM], offB[WM];
+    i64 gA[WM], gB[WM];
 };
 
-// One k-step: 64 MFMAs on `cur`, the 16 fragments of k-step `srd` of the K-tile in
-// (rdA, rdB) into `nxt`, and the 8 pieces of one unit (operand SB ? B : A at k0)
-// into `st`.  The LDS pointers are __restrict__ so the inlined accesses carry
-// alias scopes: hipcc's waitcnt pass then knows the in-flight DMA cannot alias
-// the fragment reads (without them it drains vmcnt(0) before every
+// One k-step: WM^2 MFMAs on `cur`, the 2 WM fragments of k-step `srd` of the
+// K-tile in (rdA, rdB) into `nxt`, and the WM pieces of one unit (operand SB ? B
+// : A at k0) into `st`.  The LDS pointers are __restrict__ so the inlined
+// accesses carry alias scopes: hipcc's waitcnt pass then knows the in-flight DMA
+// cannot alias the fragment reads (without them it drains vmcnt(0) before every
 // ds_read_b64_tr_b16).
-template <bool BF16, bool KCA, bool KCB, bool BUF, bool SB>
+template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool SB>
 __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
-                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const Pieces<WM>& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st, i64 k0,
-                                      f32x4 (&acc)[8][8], const Sets& cur, Sets& nxt) {
-    // Placement (measured, profiles/r03_h16_four_wave.log): the 16 fragment reads
-    // of the next k-step go out one per MFMA in the first 16 MFMAs (+1-2 % over
-    // two per 4-MFMA group in groups 0-7), the 8 staging pieces one per 4-MFMA
-    // group in groups 8-15, in both k-steps: a piece issued among the reads costs
-    // more MFMA time than the later landing of B_{t+2} (issued in the second half
-    // of (t,1), read after (t+1,0)) costs in waiting.
+                                      f32x4 (&acc)[WM][WM], const Sets<WM>& cur, Sets<WM>& nxt) {
+    constexpr int BMR = Geo<WM>::BM;
+    // Placement (measured at WM = 8, profiles/r03_h16_four_wave.log): the 2 WM
+    // fragment reads of the next k-step go out one per MFMA in the first 2 WM
+    // MFMAs, the WM staging pieces evenly over the second half of the k-step's
+    // MFMAs: a piece issued among the reads costs more MFMA time than the later
+    // landing of B_{t+2} (issued in the second half of (t,1), read after
+    // (t+1,0)) costs in waiting.
+    constexpr int NM = WM * WM, GAP = WM / 2;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int mi = q >> 1, ni = (q & 1) * 4 + t;
-            mfma_acc<BF16>(acc[mi][ni], cur.a[mi], cur.b[ni]);
-            if (t == 1 && q >= 8) {
-                const int u = q - 8;
-                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
-            }
-            const int f = 4 * q + t;  // read f: A fragments 0-7, then B 0-7
-            if (f < 16) {
-                if (f < 8) nxt.a[f] = frag<KCA>(rdA + wr * HALF, f * 16, srd, l);
-                else nxt.b[f - 8] = frag<KCB>(rdB + wc * HALF, (f - 8) * 16, srd, l);
-            }
+    for (int i = 0; i < NM; ++i) {
+        mfma_acc<BF16>(acc[i / WM][i % WM], cur.a[i / WM], cur.b[i % WM]);
+        if (i >= NM / 2 && (i - NM / 2) % GAP == 1 % GAP) {
+            const int u = (i - NM / 2) / GAP;
+            if constexpr (SB) piece<BMR, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+            else piece<BMR, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+        }
+        if (i < 2 * WM) {  // read i: A fragments 0..WM-1, then B
+            if (i < WM) nxt.a[i] = wfrag<WM, KCA>(rdA, wr, i, srd, l);
+            else nxt.b[i - WM] = wfrag<WM, KCB>(rdB, wc, i - WM, srd, l);
         }
     }
 }
 }  // namespace w4
 
 // PART: split-k partials (p.W, gridDim.y chunks), a separate instantiation so the
-// default kernel's epilogue keeps its register allocation
-template <bool BF16, bool KCA, bool KCB, bool BUF, bool PART>
-__global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
+// default kernel's epilogue keeps its register allocation.  WM = 8: one
+// workgroup per CU (the whole register file and LDS); WM = 4: two.
+template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART>
+__global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
+    constexpr int BMR = Geo<WM>::BM, UNIT = Geo<WM>::UNIT;
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
     lds_char* lds = (lds_char*)lds_raw;
 
@@ -399,7 +424,7 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
     const int wr = w >> 1, wc = w & 1;
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
-    const i64 m0 = (i64)tm * BM, n0 = (i64)tn * BN;
+    const i64 m0 = (i64)tm * BMR, n0 = (i64)tn * BMR;
     if constexpr (PART) {  // this workgroup's k chunk
         const i64 kz0 = (i64)blockIdx.y * p.kchunk;
         p.k = min(p.kchunk, p.k - kz0);
@@ -408,39 +433,40 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         p.W += (i64)blockIdx.y * p.m * p.n;
     }
 
-    Pieces pc;
+    Pieces<WM> pc;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < WM; ++u) {
         pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
         pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
         pc.offA[u] = (int)(pc.gA[u] * 2);
         pc.offB[u] = (int)(pc.gB[u] * 2);
     }
 
-    f32x4 acc[8][8];
+    f32x4 acc[WM][WM];
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+        for (int b = 0; b < WM; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / BK);
     auto kt = [&](int t) { return (i64)min(t, nt - 1) * BK; };
-        // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; fragments (0,0)
+    // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; fragments (0,0)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+        for (int u = 0; u < WM; ++u)
+            piece<BMR, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+        for (int u = 0; u < WM; ++u)
+            piece<BMR, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
     }
-    wait_cnt<16, NOWAIT_LGKM>();
+    wait_cnt<2 * WM, NOWAIT_LGKM>();
     bar8();
-    Sets X, Y;
+    Sets<WM> X, Y;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        X.a[q] = frag<KCA>(lds + wr * HALF, q * 16, 0, l);
-        X.b[q] = frag<KCB>(lds + UNIT + wc * HALF, q * 16, 0, l);
+    for (int q = 0; q < WM; ++q) {
+        X.a[q] = wfrag<WM, KCA>(lds, wr, q, 0, l);
+        X.b[q] = wfrag<WM, KCB>(lds + UNIT, wc, q, 0, l);
     }
     wait_cnt<NOWAIT_VM, 0>();
     // One K-tile; J = t % 5 makes every slot a compile-time offset of the LDS
@@ -451,13 +477,13 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
                       sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
         // (t,0): stage A_{t+2} into B_{t-1}'s slot
-        w4::kstep<BF16, KCA, KCB, BUF, false>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
-                                                 lds + st0 * UNIT, kt(t + 2), acc, X, Y);
-        wait_cnt<8, 0>();
+        w4::kstep<WM, BF16, KCA, KCB, BUF, false>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
+                                                     lds + st0 * UNIT, kt(t + 2), acc, X, Y);
+        wait_cnt<WM, 0>();
         bar8();
         // (t,1): stage B_{t+2} into A_t's slot
-        w4::kstep<BF16, KCA, KCB, BUF, true>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
-                                                lds + st1 * UNIT, kt(t + 2), acc, Y, X);
+        w4::kstep<WM, BF16, KCA, KCB, BUF, true>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+                                                    lds + st1 * UNIT, kt(t + 2), acc, Y, X);
         wait_cnt<NOWAIT_VM, 0>();
     };
     for (int t = 0; t < nt; t += NSLOT) {
@@ -468,9 +494,9 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
         if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
-    w4::settle(acc);
-    if constexpr (PART) w4::epilogue_partial(p, acc, m0, n0, wr, wc, l);
-    else w4::epilogue4<BF16>(p, acc, m0, n0, wr, wc, l);
+    w4::settle<WM>(acc);
+    if constexpr (PART) w4::epilogue_partial<WM>(p, acc, m0, n0, wr, wc, l);
+    else w4::epilogue4<BF16, WM>(p, acc, m0, n0, wr, wc, l);
 }
 
 // (Measured and removed in round 4: a two-barrier loop that keeps every wave's
@@ -478,20 +504,31 @@ __global__ __launch_bounds__(256, 1) void gemm_h4w_kernel(H2Params p) {
 // hipBLASLt's MT256x256x64 loop does — correct, but 1-6 % slower than this
 // one-barrier loop on every orientation, profiles/r04_h16_two_barrier_ab.log.)
 
-template <bool BF16, bool KCA, bool KCB>
+template <int WM, bool BF16, bool KCA, bool KCB>
 hipError_t launch_h16(const H2Params& p, hipStream_t s) {
+    constexpr int BMR = w4::Geo<WM>::BM;
     // buffer-descriptor DMA when every offset of an image fits 31 bits, else the
     // global (64-bit address) form
-    const bool buf = dma_fits(KCA ? 256 : BK, p.lda, 2) && dma_fits(KCB ? 256 : BK, p.ldb, 2);
+    const bool buf = dma_fits(KCA ? BMR : BK, p.lda, 2) && dma_fits(KCB ? BMR : BK, p.ldb, 2);
     const dim3 grid(p.tiles_m * p.tiles_n, p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
     if (p.W) {
-        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
+        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
     } else {
-        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((gemm_h4w_kernel<BF16, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
+        if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
     }
     return hipGetLastError();
+}
+
+template <int WM>
+hipError_t launch_h16_all(bool is_bf16, bool kca, bool kcb, const H2Params& p, hipStream_t s) {
+    if (is_bf16) {
+        if (kca) return kcb ? launch_h16<WM, true, true, true>(p, s) : launch_h16<WM, true, true, false>(p, s);
+        return kcb ? launch_h16<WM, true, false, true>(p, s) : launch_h16<WM, true, false, false>(p, s);
+    }
+    if (kca) return kcb ? launch_h16<WM, false, true, true>(p, s) : launch_h16<WM, false, true, false>(p, s);
+    return kcb ? launch_h16<WM, false, false, true>(p, s) : launch_h16<WM, false, false, false>(p, s);
 }
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
@@ -511,52 +548,70 @@ int GroupM() {
 
 }  // namespace
 
+// Tile size and split-k of the four-wave kernel (kernels.hpp).
+//  * 256 x 256 tiles (WM = 8) unless fewer than half the CUs would get one;
+//    then 128 x 128 tiles (WM = 4, two workgroups per CU), a grid four times as
+//    wide.  In one process against the 256-tiles (profiles/r05b_h16_sweep.log):
+//    bf16 2048^3 382 -> 673 TF (hipBLASLt 659), 2560^3 (100 tiles) 542 -> 810,
+//    1536 x 2048^2 217 -> 528, 1024^3 69 -> 177, 1024^2 x 8192 347 -> 486 (with
+//    split-k), 2048^2 x 8192 873 -> 998; but 3072^3 (144 tiles) 834 -> 768 and
+//    4096^3 (256) 1309 -> 1139: where 256-tiles fill half the chip or more, their
+//    halved LDS reads per FLOP win.  ELX_H16_TILE = 256 / 128 forces one (read
+//    per call, for A/B).
+//  * split-k where the tiles still leave at least three quarters of the CUs
+//    idle: chunks of >= 4 K-tiles (16 at 64 tiles), up to one workgroup per CU;
+//    f32 partials in the stream-ordered workspace, one reduce that applies
+//    alpha / beta and rounds once.  Round 4 with 256-tiles: bf16 1024^2 x 8192 41
+//    -> 350 TF, 2048^2 x 8192 481 -> 866; at 2560^2 (100 tiles) three chunks lost
+//    22 % and at 3072^2 (144) two lost 35 % (profiles/r04_h16_split_ab.log,
+//    r04_h16_split_ab2.log, r04_h16_split_cap_ab.log).  ELX_H16_SPLIT = z caps the
+//    chunk count (0 or 1: none).
+H16Plan h16_plan(i64 m, i64 n, i64 kmain) {
+    const char* tv = getenv("ELX_H16_TILE");
+    const int force = tv ? atoi(tv) : 0;
+    const i64 t8 = ((m + 255) / 256) * ((n + 255) / 256);
+    H16Plan pl;
+    pl.wm = force == 128 ? 4 : force == 256 ? 8 : (t8 >= 128 ? 8 : 4);
+    const i64 bm = pl.wm * 32;
+    const i64 tiles = ((m + bm - 1) / bm) * ((n + bm - 1) / bm);
+    const char* sv = getenv("ELX_H16_SPLIT");
+    const i64 split_cap = sv ? (i64)atoi(sv) : 64;
+    pl.nz = 1;
+    pl.kchunk = kmain;
+    if (split_cap > 1 && tiles <= 64 && kmain >= 8 * BK) {
+        const i64 min_kt = tiles >= 64 ? 16 : 4;
+        const i64 z = std::min<i64>(std::min<i64>((256 + tiles - 1) / tiles, kmain / (min_kt * BK)), split_cap);
+        if (z >= 2) {
+            pl.kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
+            pl.nz = (kmain + pl.kchunk - 1) / pl.kchunk;
+        }
+    }
+    return pl;
+}
+
 #ifndef ELX_KERNEL_PROBE
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
     const bool kca = ta, kcb = !tb;
     const i64 kmain = k / BK * BK;
-    // the large-tile path: 16-B aligned rows/columns for the DMA, RC operands a
-    // multiple of 8 long (whole 16-B chunks), and enough tiles to fill the chip
-    const i64 tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
-    // split-k where the tiles leave at least three quarters of the CUs idle:
-    // chunks of >= 4 K-tiles (16 at 64 tiles), up to one workgroup per CU; f32 partials in the
-    // stream-ordered workspace, one reduce that applies alpha / beta and rounds
-    // once.  bf16 1024^2 x 8192 41 -> 350 TF, 2048^2 x 8192 481 -> 866, 1024^3 32 ->
-    // 69, 2048^3 326 -> 381; at 2560^2 (100 tiles) three chunks lost 22 % and at
-    // 3072^2 (144) two lost 35 %, so those stay whole (profiles/r04_h16_split_ab.log,
-    // r04_h16_split_ab2.log).  ELX_H16_SPLIT = z caps the chunk count (0 or 1: none).
-    static const i64 split_cap = [] { const char* v = getenv("ELX_H16_SPLIT"); return v ? (i64)atoi(v) : (i64)64; }();
-    i64 nz = 1, kchunk = kmain;
-    if (split_cap > 1 && tiles <= 64 && kmain >= 8 * BK) {
-        // chunks of >= 16 K-tiles at 64 tiles, where the partials' traffic is
-        // m n z words against k / z of MFMAs (2048^3: 2 chunks 381 TF, 4 chunks
-        // 359; 2048^2 x 8192: 4 chunks 857, 2: 756; profiles/r04_h16_split_cap_ab.log)
-        const i64 min_kt = tiles >= 64 ? 16 : 4;
-        const i64 z = std::min<i64>(std::min<i64>((256 + tiles - 1) / tiles, kmain / (min_kt * BK)), split_cap);
-        if (z >= 2) {
-            kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
-            nz = (kmain + kchunk - 1) / kchunk;
-        }
-    }
+    const H16Plan pl = h16_plan(m, n, kmain);
+    const int BMR = pl.wm * 32;
+    const i64 tiles = ((m + BMR - 1) / BMR) * ((n + BMR - 1) / BMR);
+    // the LDS-DMA path: 16-B aligned rows/columns for the DMA, RC operands a
+    // multiple of 8 long (whole 16-B chunks), and enough workgroups
     const bool ok = kmain > 0 && al16(A) && al16(B) && lda % 8 == 0 && ldb % 8 == 0 &&
-                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) && tiles * nz >= 64 &&
+                    (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) && tiles * pl.nz >= 64 &&
                     m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
-    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BM - 1) / BM), (int)((n + BN - 1) / BN),
-               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), kchunk, nullptr};
+    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BMR - 1) / BMR), (int)((n + BMR - 1) / BMR),
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), pl.kchunk, nullptr};
+    const i64 nz = pl.nz;
     hipError_t e;
     if (nz > 1) {
         e = workspace_alloc(reinterpret_cast<void**>(&p.W), sizeof(float) * (size_t)m * (size_t)n * (size_t)nz, s);
         if (e != hipSuccess) return e;
     }
-    if (is_bf16) {
-        if (kca) e = kcb ? launch_h16<true, true, true>(p, s) : launch_h16<true, true, false>(p, s);
-        else e = kcb ? launch_h16<true, false, true>(p, s) : launch_h16<true, false, false>(p, s);
-    } else {
-        if (kca) e = kcb ? launch_h16<false, true, true>(p, s) : launch_h16<false, true, false>(p, s);
-        else e = kcb ? launch_h16<false, false, true>(p, s) : launch_h16<false, false, false>(p, s);
-    }
+    e = pl.wm == 8 ? launch_h16_all<8>(is_bf16, kca, kcb, p, s) : launch_h16_all<4>(is_bf16, kca, kcb, p, s);
     if (nz > 1) {
         if (e == hipSuccess) {
             const i64 mn = m * n;

@@ -96,6 +96,10 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
 hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchunk, float alpha, const float* A,
                             i64 lda, const float* B, i64 ldb, float beta, float* C, i64 ldc, hipStream_t s);
 // 16-bit GEMMs: is_bf16 selects bf16 vs f16 storage; f32 accumulation.
+// the 16-bit four-wave kernel's plan (gemm_h16.hip): tile 32 wm (wm 8 or 4),
+// nz split-k chunks of kchunk (nz = 1: whole k)
+struct H16Plan { int wm; i64 nz, kchunk; };
+H16Plan h16_plan(i64 m, i64 n, i64 kmain);
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
                        const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
                        uint16_t* C, i64 ldc, hipStream_t s);

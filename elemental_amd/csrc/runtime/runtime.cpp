@@ -70,25 +70,10 @@ void Runtime::EnsureGPU() {
     // (ELX_COMM_PRIORITY=0: the compute stream's priority instead; A/B timing)
     const char* pe = getenv("ELX_COMM_PRIORITY");
     ELX_CHECK_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, pe && atoi(pe) == 0 ? lo : hi));
-    ELX_CHECK_HIP(hipStreamCreateWithFlags(&release_, hipStreamNonBlocking));
-    // The library's own backing pool: other default-pool users of the process
-    // (RCCL, the caller's hipMallocAsync) never share its blocks, and every
-    // reuse decision is the cache's (runtime.hpp): the driver's reuse policies
-    // are off, and the pool keeps what it is given back (threshold = max;
-    // ELX_POOL_RELEASE_THRESHOLD overrides it for tests) until a trim.
-    hipMemPoolProps props{};
-    props.allocType = hipMemAllocationTypePinned;
-    props.handleTypes = hipMemHandleTypeNone;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = device_;
-    ELX_CHECK_HIP(hipMemPoolCreate(&pool_, &props));
-    uint64_t thresh = std::numeric_limits<uint64_t>::max();
-    if (const char* e = std::getenv("ELX_POOL_RELEASE_THRESHOLD")) thresh = std::strtoull(e, nullptr, 10);
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolAttrReleaseThreshold, &thresh));
-    int off = 0;
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseFollowEventDependencies, &off));
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowOpportunistic, &off));
-    ELX_CHECK_HIP(hipMemPoolSetAttribute(pool_, hipMemPoolReuseAllowInternalDependencies, &off));
+    // The cache's backing store is hipMalloc / hipFree, as hipCUB's
+    // CachingDeviceAllocator's is (cudaMalloc / cudaFree): the driver's
+    // stream-ordered pool (hipMallocFromPoolAsync) was measured to corrupt live
+    // blocks on this ROCm (runtime.hpp, tools/pool_trim_probe.hip).
     if (!max_cached_set_) {
         // H_CUB_MAX_CACHED_SIZE as the reference reads it (cub.cpp:37-43)
         for (const char* v : {"ELX_POOL_MAX_CACHED", "H_CUB_MAX_CACHED_SIZE"}) {
@@ -177,15 +162,13 @@ hipEvent_t Runtime::EventLocked() {
     return ev;
 }
 
-void* Runtime::Backing(size_t bin, hipStream_t s) {
+void* Runtime::Backing(size_t bin, hipStream_t) {
     void* p = nullptr;
-    hipError_t e = hipMallocFromPoolAsync(&p, bin, pool_, s);
+    hipError_t e = hipMalloc(&p, bin);
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
         (void)hipGetLastError();
         ReleaseCachedLocked(0);  // give the cache back and retry once
-        ELX_CHECK_HIP(hipDeviceSynchronize());
-        ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
-        e = hipMallocFromPoolAsync(&p, bin, pool_, s);
+        e = hipMalloc(&p, bin);
     }
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -194,19 +177,17 @@ void* Runtime::Backing(size_t bin, hipStream_t s) {
         throw HIPError(Cat("elx_pool_alloc: ", hipGetErrorString(e), " (", bin, " bytes requested, ",
                            fr, " bytes available, ", tot, " bytes total, ", cached_, " cached)"));
     }
+    backing_ += bin;
     return p;
 }
 
 void Runtime::ReturnLocked(void* p, size_t bin, hipEvent_t ready) {
-    // The block's last use must be complete before the backing pool sees it
-    // (the pool may re-back or hand out a freed block before queued work on it
-    // runs: runtime.hpp).  So: the host waits for the free's event, the block is
-    // freed on the private, idle release stream, and the pool trimmed to what
-    // is still allocated from it, as CUB's synchronous cudaFree returns memory.
+    // The block's last use is complete before the driver sees it again: the
+    // host waits for the free's event (hipFree synchronizes as well), as CUB's
+    // DeviceFree returns over-cap blocks with a synchronous cudaFree.
     ELX_CHECK_HIP(hipEventSynchronize(ready));
-    ELX_CHECK_HIP(hipFreeAsync(p, release_));
-    ELX_CHECK_HIP(hipStreamSynchronize(release_));
-    ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
+    ELX_CHECK_HIP(hipFree(p));
+    backing_ -= bin;
     spare_events_.push_back(ready);
     if (Bins().debug)
         std::fprintf(stderr, "elx_pool[dev %d]: returned block %p (%zu bytes) to the driver (cached %zu, live %zu)\n",
@@ -310,8 +291,6 @@ void Runtime::Trim(size_t keep) {
     ELX_CHECK_HIP(hipDeviceSynchronize());
     std::lock_guard<std::mutex> lk(mu_);
     ReleaseCachedLocked(keep);
-    ELX_CHECK_HIP(hipDeviceSynchronize());
-    ELX_CHECK_HIP(hipMemPoolTrimTo(pool_, 0));
 }
 
 void Runtime::SetMaxCached(size_t bytes) {
@@ -334,10 +313,7 @@ void Runtime::Stats(size_t& reserved, size_t& in_use) {
 
 size_t Runtime::BackingReserved() {
     std::lock_guard<std::mutex> lk(mu_);
-    if (!gpu_ready_) return 0;
-    uint64_t v = 0;
-    ELX_CHECK_HIP(hipMemPoolGetAttribute(pool_, hipMemPoolAttrReservedMemCurrent, &v));
-    return static_cast<size_t>(v);
+    return backing_;
 }
 
 namespace kern {

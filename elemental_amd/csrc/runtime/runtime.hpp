@@ -21,22 +21,23 @@
 //    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE); a
 //    block that does not fit under the cap, an uncacheable block and, with
 //    ELX_POOL_CACHE=0, every block leaves the allocator: the host waits for its
-//    free's event, gives it back to the backing pool and trims the pool, so
-//    the memory returns to the driver (CUB's synchronous cudaFree);
-//  * the backing store is the library's own hipMemPool (hipMemPoolCreate),
-//    never the device's default pool shared with other users of the process.
-//    It only ever receives IDLE blocks (their last use complete on the host's
-//    view) and decides no reuse itself: its reuse policies are off and its
-//    release threshold is max (ELX_POOL_RELEASE_THRESHOLD overrides, for
-//    tests).  Round 5 measured why (tools/pool_race_probe.hip,
-//    profiles/r05_pool_race_probe.log): on this ROCm a hipFreeAsync'd block whose
-//    earlier work is still queued can be re-backed or handed out before that
-//    work runs (readers saw zero pages or the next owner's data), and with
+//    free's event and hipFrees it, so the memory returns to the driver (CUB's
+//    synchronous cudaFree);
+//  * the backing store is hipMalloc / hipFree, as under hipCUB's
+//    CachingDeviceAllocator (cudaMalloc / cudaFree); a block goes back to the
+//    driver only once the host has seen its free's event complete.  Not the
+//    driver's stream-ordered pool (hipMallocFromPoolAsync): round 5 measured it
+//    on this ROCm (tools/pool_race_probe.hip, tools/pool_trim_probe.hip,
+//    profiles/r05_pool_probes.log): a hipFreeAsync'd block whose earlier work
+//    is still queued is re-backed or handed out before that work runs; with
 //    follow-event-dependencies on, a stream that once waited on an OLDER event
-//    of the freeing stream receives the block at once.  Every device scratch of
-//    the library (the split-k partials too, kern::workspace_alloc) comes from
-//    this allocator; a failed backing allocation releases the cache and retries
-//    once before reporting out-of-memory;
+//    of the freeing stream receives the block at once; and even with every
+//    free idle, single-stream and the release threshold at max, allocations
+//    after frees overwrote blocks that were still live (hipMalloc: clean on the
+//    same sequence).  Every device scratch of the library (the split-k
+//    partials too, kern::workspace_alloc) comes from this allocator; a failed
+//    backing allocation releases the cache and retries once before reporting
+//    out-of-memory;
 //  * H_CUB_DEBUG=1 (cub.cpp:45-50) logs every allocation, reuse (with the
 //    stream it was freed on and the event the new stream waits on), cache
 //    return and release to stderr.
@@ -71,8 +72,8 @@ public:
     void Trim(size_t keep);
     // reserved = live + cached bin bytes; in_use = requested bytes still live
     void Stats(size_t& reserved, size_t& in_use);
-    // what the backing hipMemPool itself holds from the driver
-    // (hipMemPoolAttrReservedMemCurrent; 0 before the first GPU use)
+    // bytes held from the driver (hipMalloc'd, not yet hipFree'd): live +
+    // cached blocks; 0 before the first GPU use
     size_t BackingReserved();
     void SetMaxCached(size_t bytes);
     size_t MaxCached();
@@ -86,20 +87,18 @@ private:
     Runtime() = default;
     void* Backing(size_t bin, hipStream_t s);
     void ReleaseCachedLocked(size_t keep);
-    // give an idle-to-be block back to the backing pool: the host waits for
-    // `ready`, frees it on the private release stream and trims the pool
+    // give a block back to the driver once the host saw `ready` complete
     void ReturnLocked(void* p, size_t bin, hipEvent_t ready);
     hipEvent_t EventLocked();
     std::mutex mu_;
     bool gpu_ready_ = false;
     int device_ = -1;
     int reserved_cus_ = 0;
-    hipStream_t compute_ = nullptr, comm_ = nullptr, release_ = nullptr;
-    hipMemPool_t pool_ = nullptr;
+    hipStream_t compute_ = nullptr, comm_ = nullptr;
     std::unordered_map<void*, Live> live_;
     std::multimap<size_t, Cached> cache_;  // bin bytes -> freed block
     std::vector<hipEvent_t> spare_events_;
-    size_t in_use_ = 0, live_bin_ = 0, cached_ = 0;
+    size_t in_use_ = 0, live_bin_ = 0, cached_ = 0, backing_ = 0;
     size_t max_cached_ = ~size_t(0);
     bool max_cached_set_ = false;
 };

@@ -542,7 +542,7 @@ def pool_stats() -> tuple[int, int]:
 
 
 def pool_backing_reserved() -> int:
-    """Bytes the allocator's backing hipMemPool holds from the driver."""
+    """Bytes the allocator holds from the driver (live + cached blocks)."""
     r = c_size_t()
     call("elx_pool_backing_reserved", byref(r))
     return r.value

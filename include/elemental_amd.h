@@ -148,9 +148,8 @@ size_t elx_pool_bin_bytes(size_t bytes);
 /* 1 when a request of `bytes` is cached on free, 0 when it is above
  * H_CUB_MAX_BIN's bin (an own-size block returned to the driver on free) */
 int elx_pool_bin_cacheable(size_t bytes);
-/* bytes the backing hipMemPool holds from the driver
- * (hipMemPoolAttrReservedMemCurrent): live + cached blocks once blocks that
- * left the cache were trimmed back */
+/* bytes the allocator holds from the driver (hipMalloc'd, not yet hipFree'd):
+ * its live and cached blocks */
 int elx_pool_backing_reserved(size_t* bytes);
 int elx_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int elx_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);

@@ -547,14 +547,14 @@ def test_gpu_symm_distributed(world, height):
     _spawn(W.symm_worker, world, height, el.GPU, el.F64, 45, 29, 61)
 
 
-@pytest.mark.parametrize("threshold", [None, "0"])
-def test_gpu_gemm_suite_driver(tmp_path, threshold):
+@pytest.mark.parametrize("cache", [None, "0"])
+def test_gpu_gemm_suite_driver(tmp_path, cache):
     """The reference suite's experiment files run unchanged through the drop-in
     header on Device::GPU (tests/cpp/gemm_suite.cpp): every algorithm id,
     double / float / half / bfloat16, warm-up associativity residuals enforced
     (--check), one results line per experiment in the suite's format.  Also with
-    the backing pool's release threshold at 0 (ELX_POOL_RELEASE_THRESHOLD=0),
-    the setting under which round 4 saw wrong products on the second warm-up
+    the allocator's cache off (ELX_POOL_CACHE=0: every block returns to the
+    driver at its free), where round 4 saw wrong products on the second warm-up
     (DESIGN.md section 2)."""
     import os
     import subprocess
@@ -569,9 +569,9 @@ def test_gpu_gemm_suite_driver(tmp_path, threshold):
     exp.write_text("\n".join(lines) + "\n")
     res = tmp_path / "res.txt"
     env = dict(os.environ)
-    if threshold is not None:
-        env["ELX_POOL_RELEASE_THRESHOLD"] = threshold
-    r = subprocess.run([exe, "--f", str(exp), "--o", str(res), "--warmup", "3" if threshold else "2", "--runs", "3",
+    if cache is not None:
+        env["ELX_POOL_CACHE"] = cache
+    r = subprocess.run([exe, "--f", str(exp), "--o", str(res), "--warmup", "3" if cache else "2", "--runs", "3",
                         "--check"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     out = res.read_text().splitlines()

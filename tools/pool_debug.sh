@@ -1,13 +1,11 @@
 #!/bin/bash
-# gemm_suite repeated with the backing pool's release threshold at 0
-# (ELX_POOL_RELEASE_THRESHOLD=0) and under the allocator's debug knobs: the
-# round-4 wrong-result hunt (intermittent associativity residuals 0.05-5 on the
-# second warm-up with threshold-0 pools).  Usage: tools/pool_debug.sh [reps]
+# gemm_suite repeated under the allocator's debug knobs: the round-4
+# wrong-result hunt (intermittent associativity residuals 0.05-5 on the second
+# warm-up, with the cache off too).  Usage: tools/pool_debug.sh [reps]
 S=tests/cpp/_build/gemm_suite
 REPS=${1:-3}
 fails=0
-for v in "ELX_POOL_RELEASE_THRESHOLD=0" "ELX_POOL_RELEASE_THRESHOLD=0 ELX_POOL_CACHE=0" \
-         "ELX_POOL_RELEASE_THRESHOLD=0 ELX_POOL_POISON=1"; do
+for v in "ELX_POOL_CACHE=1" "ELX_POOL_CACHE=0" "ELX_POOL_POISON=1"; do
   for rep in $(seq 1 "$REPS"); do
     for f in tools/suite_pool_exp.txt tools/suite_pool_exp2.txt; do
       echo "=== env [$v] rep $rep exp $f"
