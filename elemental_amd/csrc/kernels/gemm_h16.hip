@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <utility>
 #include "kernels.hpp"
@@ -61,6 +62,8 @@ struct H2Params {
     int tiles_m, tiles_n;
     int vec_c;    // C base 8-B aligned and ldc % 4 == 0
     int group_m;  // tile-order group height (ELX_H16_GROUP, default 8)
+    int sblock;   // 1: super-block order (tile_of_sb); needs the grid to be whole super-blocks
+    int sb_xr, sb_pr;  // its geometry
     // split-k (gridDim.y chunks, W != null): chunk z covers k in [z*kchunk,
     // min(k, (z+1)*kchunk)) and writes its raw f32 product to W + z*m*n (ld m);
     // h16_splitk_reduce applies alpha / beta and rounds once
@@ -78,6 +81,23 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
     const int inner = wg - group * per_group;
     tm = first_m + inner % gsz;
     tn = inner / gsz;
+}
+
+// Super-block order: the 256 workgroups that run at once (one per CU) cover one
+// 16 x 16 block of tiles, each XCD an 8 x 4 part of it (bid & 7 is the XCD a
+// workgroup is dispatched to, bid >> 3 its turn there: 32 at a time).  An XCD's
+// L2 sees the same 8 + 4 operand slices per K-tile as in tile_of's grouped
+// order, but the eight XCDs now read 16 A and 16 B slices between them instead
+// of 64 A and 4 B, so the Infinity Cache serves what one XCD fetched to the
+// others and HBM reads less per launch.
+// Geometry: the XCDs form an xr x (8 / xr) grid of parts of pr x (32 / pr)
+// tiles each (default 2 x 4 parts of 8 x 4).
+__device__ __forceinline__ void tile_of_sb(int bid, int tiles_n, int xr, int pr, int& tm, int& tn) {
+    const int xcd = bid & 7, i = bid >> 3, r = i >> 5, s = i & 31;
+    const int pc = 32 / pr, sbr = xr * pr, sbc = (8 / xr) * pc;
+    const int sbn = tiles_n / sbc;
+    tm = (r / sbn) * sbr + (xcd % xr) * pr + (s % pr);
+    tn = (r % sbn) * sbc + (xcd / xr) * pc + (s / pr);
 }
 
 // XOR swizzles (16-B chunk index).  KC: 8 chunks per 128-B row, row r -> c ^ ((r>>1)&7):
@@ -423,7 +443,8 @@ __global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 1, wc = w & 1;
     int tm, tn;
-    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    if (p.sblock) tile_of_sb(blockIdx.x, p.tiles_n, p.sb_xr, p.sb_pr, tm, tn);
+    else tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
     const i64 m0 = (i64)tm * BMR, n0 = (i64)tn * BMR;
     if constexpr (PART) {  // this workgroup's k chunk
         const i64 kz0 = (i64)blockIdx.y * p.kchunk;
@@ -603,8 +624,28 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                     (kca || (m % 8 == 0 && m >= 8)) && (kcb || (n % 8 == 0 && n >= 8)) && tiles * pl.nz >= 64 &&
                     m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
-    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, (int)((m + BMR - 1) / BMR), (int)((n + BMR - 1) / BMR),
-               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), pl.kchunk, nullptr};
+    const int tm_ = (int)((m + BMR - 1) / BMR), tn_ = (int)((n + BMR - 1) / BMR);
+    // The super-block order (tile_of_sb) for grids of whole super-blocks at one
+    // workgroup per CU; in one process against the grouped order
+    // (profiles/r05f_h16_map_ab.log, r05f_h16_map_sweep.log): bf16 TN 16384^3
+    // 1478 -> 1520 TF and 1319 -> 1515 on a box where the grouped order ran
+    // slow, NN 16384^3 +3 %, NN 32768^3 within +-1.6 %; 2 x 4 XCD parts of 8 x 4
+    // tiles were the best of six geometries.  ELX_H16_MAP = 0 turns it off,
+    // ELX_H16_SB = "xr,pr" sets the geometry (both read per call, for A/B).
+    const char* sbv = getenv("ELX_H16_MAP");
+    int xr = 2, pr = 8;
+    if (const char* g = getenv("ELX_H16_SB")) {
+        int a = 0, b = 0;
+        if (sscanf(g, "%d,%d", &a, &b) == 2 && a >= 1 && a <= 8 && 8 % a == 0 && b >= 1 && b <= 32 && 32 % b == 0) {
+            xr = a;
+            pr = b;
+        }
+    }
+    const int sbr = xr * pr, sbc = (8 / xr) * (32 / pr);
+    const int sblock = !(sbv && atoi(sbv) == 0) && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
+    H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, tm_, tn_,
+               (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), sblock, xr, pr, pl.kchunk,
+               nullptr};
     const i64 nz = pl.nz;
     hipError_t e;
     if (nz > 1) {

@@ -227,7 +227,7 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64), (1024, 1024, 8192),
-                                   (1002, 1032, 4096), (2048, 2048, 2112), (1536, 2312, 704)])
+                                   (1002, 1032, 4096), (2048, 2048, 2112), (1536, 2312, 704), (4096, 4096, 192)])
 def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     """Integer operands in [-2, 2]: every partial sum is exact in the f32
     accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
@@ -241,8 +241,9 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     partials' scalar stores; TN / TT only, the others take the simple kernel).
     `tile`: the four-wave kernel's tile as the plan picks it (""), or forced to
     128 x 128 / 256 x 256 (ELX_H16_TILE), so both instantiations see every
-    shape.  (k a multiple of 64: a k tail is a second pass that adds to the
-    already rounded C.)"""
+    shape.  (4096, 4096, 192): a 16 x 16 grid of 256-tiles, run in the
+    super-block tile order (tile_of_sb).  (k a multiple of 64: a k tail is a
+    second pass that adds to the already rounded C.)"""
     if tile:
         monkeypatch.setenv("ELX_H16_TILE", tile)
     m, n, k = shape
