@@ -625,13 +625,17 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                     m < (1ll << 31) && n < (1ll << 31);
     if (!ok) return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
     const int tm_ = (int)((m + BMR - 1) / BMR), tn_ = (int)((n + BMR - 1) / BMR);
-    // The super-block order (tile_of_sb) for grids of whole super-blocks at one
-    // workgroup per CU; in one process against the grouped order
-    // (profiles/r05f_h16_map_ab.log, r05f_h16_map_sweep.log): bf16 TN 16384^3
-    // 1478 -> 1520 TF and 1319 -> 1515 on a box where the grouped order ran
-    // slow, NN 16384^3 +3 %, NN 32768^3 within +-1.6 %; 2 x 4 XCD parts of 8 x 4
-    // tiles were the best of six geometries.  ELX_H16_MAP = 0 turns it off,
-    // ELX_H16_SB = "xr,pr" sets the geometry (both read per call, for A/B).
+    // The super-block order (tile_of_sb) for grids of whole super-blocks of at
+    // most 64 x 64 tiles, one workgroup per CU.  In one process against the
+    // grouped order (profiles/r05f_h16_map_ab.log, r05f_h16_map_sweep.log,
+    // r05k_map_ab.log): bf16 TN 16384^3 +2.7-15 % (1478 -> 1520 TF; 1319 -> 1515
+    // on a box where the grouped order ran slow), NN 16384^3 +3-4 %; 2 x 4 XCD
+    // parts of 8 x 4 tiles was the best of six geometries.  At 32768^3 (C5) it
+    // is even to -1.6 % and reads 1.6x the grouped order's bytes over the fabric
+    // (L2 hit 72 vs 81 %, profiles/r05j_c5_pmc.json vs r05j_c5m0_pmc.json), so
+    // larger grids keep the grouped order.  ELX_H16_MAP = 0 / 1 forces the
+    // grouped / super-block order, ELX_H16_SB = "xr,pr" sets the geometry (both
+    // read per call, for A/B).
     const char* sbv = getenv("ELX_H16_MAP");
     int xr = 2, pr = 8;
     if (const char* g = getenv("ELX_H16_SB")) {
@@ -642,7 +646,8 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
         }
     }
     const int sbr = xr * pr, sbc = (8 / xr) * (32 / pr);
-    const int sblock = !(sbv && atoi(sbv) == 0) && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
+    const int mode = sbv ? atoi(sbv) : ((i64)tm_ * tn_ <= 4096 ? 1 : 0);
+    const int sblock = mode == 1 && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, tm_, tn_,
                (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), sblock, xr, pr, pl.kchunk,
                nullptr};

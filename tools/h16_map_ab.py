@@ -33,7 +33,7 @@ def run(spec, reps, maps):
     for _ in range(reps):
         for mp in maps:
             if mp == "0":
-                os.environ["ELX_H16_MAP"] = "0"
+                os.environ["ELX_H16_MAP"] = mp
             else:
                 os.environ["ELX_H16_MAP"] = "1"
                 os.environ["ELX_H16_SB"] = mp
