@@ -5,5 +5,5 @@
 # usage: tools/rehearse_nranks.sh N [bench args...]
 N=$1; shift
 export ELX_BENCH_COMM=host
-exec python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
+python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
   --master-port $((29500 + N)) bench.py --gpus "$N" "$@"
