@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 #include "kernels.hpp"
 #include "lds_dma.hpp"
 
@@ -244,6 +245,236 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
         }
 }
 
+// ---------------------------------------------------------------------------
+// Ring kernel (round 5): the 16-bit four-wave loop (gemm_h16.hip) in fp64.
+// 128 x 128 tile, four waves of 64 x 64 (4 x 4 accumulators of
+// v_mfma_f64_16x16x4_f64, 64 cycles each), one wave per SIMD, one workgroup per
+// CU.  Staging unit = one operand's K-tile image of RBK = 32 k (KC: 128 rows of
+// 256 B; RC: 32 k-rows of 1 KiB): 32 KiB = 32 one-KiB pieces, 8 per wave; a ring
+// of 5 slots (160 KiB): A_t is unit 2t, B_t unit 2t+1, unit u in slot u % 5.
+// A K-tile is 8 k-steps of 16 MFMAs per wave (8192 cycles).  In K-tile t:
+//   (t,0..3): two pieces of A_{t+2} per k-step, into B_{t-1}'s slot;
+//   (t,0..6): each k-step's MFMAs and the next k-step's 8 operand reads from
+//             A_t, B_t;
+//   after (t,6): vmcnt(8) (A_{t+1}, B_{t+1} landed; A_{t+2} may be in
+//             flight), lgkmcnt(0), barrier;
+//   (t,7):    MFMAs; reads of (t+1,0) from A_{t+1}, B_{t+1}; the 8 pieces of
+//             B_{t+2} into A_t's slot.
+// RAW: A_{t+1}, B_{t+1} are read from (t,7) on, after every wave's wait and the
+// barrier.  WAR: A_t's and B_t's last reads are issued in (t,6) and retired
+// before that barrier; A_t's slot is restaged in (t,7), B_t's in (t+1,0..3),
+// both after it.  No wave can pass a barrier another has not reached, so one
+// barrier per K-tile (8192 MFMA cycles) suffices.  Units past the end re-stage
+// the last K-tile into a slot nobody reads again (counted waits stay exact).
+// Versus the two-stage slab kernel (one barrier and a full vmcnt(0) drain per
+// 16-k slab, two workgroups per CU): no drain, one barrier per 32 k, 1.5 K-tiles
+// of DMA lead.
+// ---------------------------------------------------------------------------
+namespace ring {
+constexpr int RBK = 32, NSLOT = 5, UNIT = 128 * RBK * 8, WT = 64;
+
+// per-lane element offset of piece `ins` (0..31) of one operand's K-tile image
+template <bool KC>
+__device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
+    if (KC) {  // 4 rows of 256 B per piece; chunk c of row r at c ^ (r & 15)
+        const int r = ins * 4 + (l >> 4);
+        const int c = (l & 15) ^ swz_kc<RBK>(r);
+        const i64 row = R0 + r < rows ? r : rows - 1 - R0;
+        return row * ld + 2 * c;
+    } else {   // one 1-KiB k-row per piece; chunk c at c ^ 8 (kk & 1)
+        const int kk = ins;
+        const int c = l ^ ((kk & 1) << 3);
+        const i64 col = R0 + 2 * c <= rows - 2 ? 2 * c : rows - 2 - R0;
+        return col + kk * ld;
+    }
+}
+
+template <bool BUF, bool KC>
+__device__ __forceinline__ void piece(const double* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int ins,
+                                      lds_char* img) {
+    const double* base = KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
+    if constexpr (BUF) {
+        const BufferSrc<double> src(base, (KC ? 128 : RBK) * ld * 8);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + ins * 1024),
+                                                 16, off, 0, 0, 0);
+    } else {
+        __builtin_amdgcn_global_load_lds((const void*)(base + goff),
+                                         (__attribute__((address_space(3))) void*)(img + ins * 1024), 16, 0, 0);
+    }
+}
+
+struct Ops { double a[4], b[4]; };
+// this lane's buffer offsets (bytes) / element offsets of its 8 pieces per operand
+struct Pieces { int offA[8], offB[8]; i64 gA[8], gB[8]; };
+
+// acc += a b.  The builtin, not asm: hipcc's hazard recognizer then pads the
+// operand hazards (an asm MFMA here gave wrong products on 1.4 % of the entries:
+// the wait states around its operand registers are nobody's job), and with the
+// placement pinned by sched_barrier it allocates the accumulators in place (no
+// v_accvgpr moves in the loop).
+__device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+}
+
+// one k-step: 16 MFMAs on `cur`, the next k-step's operands (k-step `srd` of the
+// K-tile in rdA / rdB) into `nxt`, and NP pieces u0.. of one unit into `st`
+template <bool KCA, bool KCB, bool BUF, bool SB, int NP>
+__device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
+                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st,
+                                      int u0, i64 k0, f64x4 (&acc)[4][4], const Ops& cur, Ops& nxt) {
+    // pieces in the second half of the MFMAs, SP apart (reads in the first half)
+    constexpr int SP = NP > 0 ? 8 / NP : 1, OFF = SP > 1 ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        mfma_acc(acc[i >> 2][i & 3], cur.a[i >> 2], cur.b[i & 3]);
+        if (i < 8) {  // the next k-step's operands, one read per MFMA
+            if (i < 4) nxt.a[i] = opnd<KCA, 128, RBK>(rdA, wr * WT + i * 16, srd, l);
+            else nxt.b[i - 4] = opnd<KCB, 128, RBK>(rdB, wc * WT + (i - 4) * 16, srd, l);
+        }
+        if constexpr (NP > 0) {
+            if (i >= 8 + OFF && (i - 8 - OFF) % SP == 0 && (i - 8 - OFF) / SP < NP) {
+                const int u = u0 + (i - 8 - OFF) / SP;
+                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the placement as written
+    }
+}
+}  // namespace ring
+
+template <bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
+    using namespace ring;
+    __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
+    lds_char* lds = (lds_char*)lds_raw;
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
+    const i64 m0 = (i64)tm * 128, n0 = (i64)tn * 128;
+    {
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += KCA ? kz0 : kz0 * p.lda;
+        p.B += KCB ? kz0 : kz0 * p.ldb;
+        p.C += (i64)blockIdx.y * p.zstride;
+    }
+    Pieces pc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.offA[u] = (int)(pc.gA[u] * 8);
+        pc.offB[u] = (int)(pc.gB[u] * 8);
+    }
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / RBK);
+    auto kt = [&](int t) { return (i64)min(t, nt - 1) * RBK; };
+    // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; operands (0,0)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+    }
+    wait_cnt<16, NOWAIT_LGKM>();
+    dma_barrier();
+    Ops X, Y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        X.a[q] = opnd<KCA, 128, RBK>(lds, wr * WT + q * 16, 0, l);
+        X.b[q] = opnd<KCB, 128, RBK>(lds + UNIT, wc * WT + q * 16, 0, l);
+    }
+    wait_cnt<NOWAIT_VM, 0>();
+    auto ktile = [&](auto jc, int t) {
+        constexpr int J = decltype(jc)::value;
+        constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
+                      sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
+        lds_char* rA = lds + sA * UNIT;
+        lds_char* rB = lds + sB * UNIT;
+        const i64 k2 = kt(t + 2);
+        // (t,0..3): operands of (t,1..4); two pieces of A_{t+2} each
+        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 1, lds + st0 * UNIT, 0, k2, acc, X, Y);
+        wait_cnt<NOWAIT_VM, 0>();
+        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 2, lds + st0 * UNIT, 2, k2, acc, Y, X);
+        wait_cnt<NOWAIT_VM, 0>();
+        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 3, lds + st0 * UNIT, 4, k2, acc, X, Y);
+        wait_cnt<NOWAIT_VM, 0>();
+        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 4, lds + st0 * UNIT, 6, k2, acc, Y, X);
+        wait_cnt<NOWAIT_VM, 0>();
+        // (t,4..6): operands of (t,5..7), no staging
+        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 5, lds, 0, k2, acc, X, Y);
+        wait_cnt<NOWAIT_VM, 0>();
+        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 6, lds, 0, k2, acc, Y, X);
+        wait_cnt<NOWAIT_VM, 0>();
+        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 7, lds, 0, k2, acc, X, Y);
+        wait_cnt<8, 0>();
+        dma_barrier();
+        // (t,7): operands of (t+1,0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
+        ring::kstep<KCA, KCB, BUF, true, 8>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+                                            lds + st1 * UNIT, 0, k2, acc, Y, X);
+        wait_cnt<NOWAIT_VM, 0>();
+    };
+    for (int t = 0; t < nt; t += NSLOT) {
+        ktile(std::integral_constant<int, 0>{}, t);
+        if (t + 1 < nt) ktile(std::integral_constant<int, 1>{}, t + 1);
+        if (t + 2 < nt) ktile(std::integral_constant<int, 2>{}, t + 2);
+        if (t + 3 < nt) ktile(std::integral_constant<int, 3>{}, t + 3);
+        if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
+
+    // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
+    const int g = l >> 4, c = l & 15;
+    const i64 ib = m0 + wr * WT, jb = n0 + wc * WT;
+    if (m0 + 128 <= p.m && n0 + 128 <= p.n) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+            double cv[4][4];
+            if (!BETA0) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r];
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = p.alpha * acc[mi][ni][r];
+                    p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r] = BETA0 ? v : v + p.beta * cv[ni][r];
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const i64 j = jb + ni * 16 + c;
+            if (j >= p.n) continue;
+            double* col = p.C + j * p.ldc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const i64 i = ib + mi * 16 + g + 4 * r;
+                if (i < p.m) {
+                    const double v = p.alpha * acc[mi][ni][r];
+                    col[i] = BETA0 ? v : v + p.beta * col[i];
+                }
+            }
+        }
+}
+
 template <typename K>
 hipError_t launch(K kernel, dim3 grid, int nt, const GParams& p, hipStream_t s) {
     hipLaunchKernelGGL(kernel, grid, dim3(nt), 0, s, p);
@@ -268,6 +499,20 @@ hipError_t launch_g(GParams p, hipStream_t s) {
     return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
 
+template <bool KCA, bool KCB>
+hipError_t launch_r(GParams p, hipStream_t s) {
+    p.tiles_m = (int)((p.m + 127) / 128);
+    p.tiles_n = (int)((p.n + 127) / 128);
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
+    const bool buf = dma_fits(KCA ? 128 : ring::RBK, p.lda, 8) && dma_fits(KCB ? 128 : ring::RBK, p.ldb, 8);
+    if (p.beta == 0.0) {
+        if (buf) return launch(gemm_f64r_kernel<KCA, KCB, true, true>, grid, 256, p, s);
+        return launch(gemm_f64r_kernel<KCA, KCB, true, false>, grid, 256, p, s);
+    }
+    if (buf) return launch(gemm_f64r_kernel<KCA, KCB, false, true>, grid, 256, p, s);
+    return launch(gemm_f64r_kernel<KCA, KCB, false, false>, grid, 256, p, s);
+}
+
 template <typename SH>
 hipError_t launch_shape(bool kca, bool kcb, const GParams& p, hipStream_t s) {
     if (kca) return kcb ? launch_g<SH, true, true>(p, s) : launch_g<SH, true, false>(p, s);
@@ -279,9 +524,23 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 // 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU, whole k) where
 // prefer_t64 (kernels.hpp) says they balance the CUs better; ELX_F64G_T64 = 0
 // never, 2 always (tests).
+// small = 255: a grid of exactly 256 128-tiles (2048^2) takes the ring kernel,
+// which beats the eight-wave 64 x 64 tiles there (NN 64.1 -> 69.3 TF, TN 63.3 ->
+// 70.9; profiles/r05o_ring_ab.log).
 bool t64_tiles(i64 m, i64 n) {
     static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
-    return prefer_t64(v, m, n, 256);
+    return prefer_t64(v, m, n, 255);
+}
+
+// the ring kernel (128 x 128 tiles, 32-deep K-tiles) on every 128-tile grid;
+// ELX_F64G_RING = 0 falls back to the two-stage slab kernel (read per call, for
+// the A/B and the tests).  Measured against the slab kernel in one process
+// (profiles/r05o_ring_ab.log): 32768^3 NN 73.7 -> 74.0 TF, 16384^3 NN / TN / NT /
+// TT 73.8 / 68.7 / 71.9 / 73.1 -> 74.6 / 76.1 / 72.6 / 74.3, 4096^3 70.4 -> 72.1.
+bool ring_tiles(i64 m, i64 n) {
+    const char* e = getenv("ELX_F64G_RING");
+    const int v = e ? atoi(e) : 1;
+    return v == 1 && !t64_tiles(m, n);
 }
 
 }  // namespace
@@ -292,6 +551,7 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
                     (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
     if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
+    if (ring_tiles(m, n)) return dma_plan(ok && k >= ring::RBK, (m + 127) / 128 * ((n + 127) / 128), k, ring::RBK);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 
@@ -312,6 +572,10 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // TT 65.0 vs 62.2); profiles/r04_t64_waves8_ab.log (the fp32 kernel measured
     // 4-13 % slower with eight and keeps four).  ELX_F64G_T64W = 4 / 8 forces one.
     static const int t64w = [] { const char* v = getenv("ELX_F64G_T64W"); return v ? atoi(v) : 0; }();
+    if (ring_tiles(m, n) && kmain % ring::RBK == 0 && kchunk % ring::RBK == 0) {
+        if (ta) return !tb ? launch_r<true, true>(p, s) : launch_r<true, false>(p, s);
+        return !tb ? launch_r<false, true>(p, s) : launch_r<false, false>(p, s);
+    }
     if (t64_tiles(m, n)) {
         if (t64w == 8 || (t64w != 4 && !ta)) return launch_shape<Shape<64, 32, BK, 64, 16>>(ta, !tb, p, s);
         return launch_shape<Shape<64, 32, BK, 64, 32>>(ta, !tb, p, s);

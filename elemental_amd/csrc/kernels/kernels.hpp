@@ -77,9 +77,10 @@ inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
 // (576 vs 2304: fp64 51.8 -> 67.0 TF, fp32 109 -> 132), 3584^2; not 2048^2,
 // 4096^2 or any other multiple of 256 128-tiles.  mode: 0 never, 2 always
 // (tests), else this rule.  small: the largest 128-tile count that always takes
-// 64 x 64 tiles (fp32 255; fp64 256, where its eight-wave 64 x 64 tiles beat the
-// one-workgroup-per-CU 128 x 128 grid at 2048^2 in every orientation: NN 64.0 ->
-// 66.2 TF, profiles/r04_t64_waves8_ab.log).
+// 64 x 64 tiles (255 for both: round 4 sent fp64's 2048^2 grid of 256 tiles to
+// its eight-wave 64 x 64 tiles, which beat the slab kernel's 128 x 128 there,
+// NN 64.0 -> 66.2 TF; the round-5 ring kernel beats both, 69.3 TF,
+// profiles/r05o_ring_ab.log).
 inline bool prefer_t64(int mode, i64 m, i64 n, i64 small = 255) {
     if (mode == 0 || mode == 2) return mode == 2;
     const i64 t128 = (m + 127) / 128 * ((n + 127) / 128), t64 = (m + 63) / 64 * ((n + 63) / 64);

@@ -155,6 +155,40 @@ def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
     assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * (opA @ opB) - C)
 
 
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+@pytest.mark.parametrize("shape,beta", [((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0), ((2048, 4096, 2072), -1.0),
+                                        ((4096, 2048, 32), 0.5)])
+@pytest.mark.parametrize("ring", ["1", "0"])
+def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
+    """The fp64 ring kernel (gemm_f64r_kernel: four waves, a 5-slot LDS ring of
+    32-deep K-tiles; ELX_F64G_RING=1) on 128-tile grids: many wraps of the ring
+    (k = 640: 20 K-tiles), ragged edge tiles with beta = 0 (C holds NaN and must
+    not be read), the k % 32 tail through the general kernel (2072 = 64 x 32 +
+    24), and a single K-tile (k = 32: prologue and clamped restaging only).
+    Integer operands: exact in every orientation.  ring = "0": the same cases
+    through the two-stage slab kernel it replaced as the default."""
+    monkeypatch.setenv("ELX_F64G_RING", ring)
+    m, n, k = shape
+    rng = np.random.default_rng(m + k)
+    A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
+    B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(np.float64))
+    C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(np.float64))
+    C0 = C.copy()
+    if beta == 0.0:
+        C0[:] = np.nan
+    dA, dB, dC = dev(A), dev(B), dev(C0)
+    torch.cuda.synchronize()
+    L.call("elx_gemm_f64", OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0],
+           beta, dC.data_ptr(), m, None)
+    sync()
+    opA = A if ta == "N" else A.T
+    opB = B if tb == "N" else B.T
+    want = 2.0 * (opA @ opB) + (beta * C if beta != 0.0 else 0.0)
+    got = host(dC, (m, n), np.float64)
+    assert np.array_equal(got, want), f"{int(np.count_nonzero(got != want))} mismatches"
+
+
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
