@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 #include "kernels.hpp"
 #include "lds_dma.hpp"
 
@@ -259,6 +261,303 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f32g_kernel(FParams p) 
         }
 }
 
+// ---------------------------------------------------------------------------
+// Ring kernel (round 5; the fp32 form of gemm_f64g.hip's gemm_f64r_kernel): one
+// workgroup per CU, a BT x BT tile of four waves (2 x 2) of BT/2 x BT/2, and a
+// 5-slot LDS ring of K-tiles of RBK k whose operand images are 32 KiB each
+// (BT 128 with RBK 64 for grids of many tiles, BT 64 with RBK 128 for grids of
+// few).  One barrier per K-tile (8192 MFMA cycles at BT 128, 4096 at BT 64), no
+// vmcnt(0) drain, the next K-tile and half of the one after in flight.
+// K permutation: in k-step s (0..RBK/4-1) lane group g = lane>>4 supplies
+// k = (RBK/4) g + s for A and B alike, so a lane's four k-steps of one "quad"
+// are four consecutive k of its row: one ds_read_b128 per fragment and quad for
+// a k-contiguous (KC) image, four ds_read_b32 for a rows-contiguous (RC) one.
+// Swizzles (16-B chunk index): KC row r: c ^ (r & 15); RC k-row kk: c ^ 4 g(kk)
+// with g(kk) = kk / (RBK/4) the lane group reading it.  Both conflict-free: the
+// 16 lanes of a group read 16 distinct chunks mod 16 (KC) / one 64-B window, the
+// four groups in four different windows (RC).
+// K-tile t (NQ = RBK/16 quads of 4 k-steps; each quad's MFMAs run on operands
+// read during the previous quad):
+//   quads 0..NQ/2-1: the 8 pieces of A_{t+2} per wave, into B_{t-1}'s slot;
+//   quads 0..NQ-2:   MFMAs, reads of the next quad from A_t, B_t;
+//   after NQ-2:      vmcnt(8) (A_{t+1}, B_{t+1} landed), lgkmcnt(0), barrier;
+//   quad NQ-1:       MFMAs, reads of quad (t+1, 0) from A_{t+1}, B_{t+1}, the 8
+//                    pieces of B_{t+2} into A_t's slot.
+// The hazard argument is gemm_f64r_kernel's (gemm_f64g.hip).
+// ---------------------------------------------------------------------------
+namespace fring {
+constexpr int NSLOT = 5, UNIT = 32 * 1024;
+template <int BT>
+struct G {
+    static constexpr int RBK = UNIT / 4 / BT, WT = BT / 2, MI = WT / 16, NQ = RBK / 16, KS = RBK / 4;
+    static constexpr int NM = 4 * MI * MI, NR = 2 * MI;  // MFMAs and fragment reads per quad
+};
+__device__ __forceinline__ int swz_r(int r) { return r & 15; }
+template <int RBK>
+__device__ __forceinline__ int swz_k(int kk) { return ((kk / (RBK / 4)) & 3) << 2; }
+
+// per-lane element offset of piece `ins` (0..31) of one operand's K-tile image
+template <int BT, bool KC>
+__device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
+    constexpr int RBK = G<BT>::RBK;
+    if (KC) {  // rows of RBK floats; RPI rows per 1-KiB piece
+        constexpr int CPR = RBK / 4, RPI = 64 / CPR;
+        const int r = ins * RPI + l / CPR;
+        const int c = (l % CPR) ^ swz_r(r);
+        const i64 row = R0 + r < rows ? r : rows - 1 - R0;
+        return row * ld + 4 * c;
+    } else {   // k-rows of BT floats; KPI k-rows per piece
+        constexpr int CPK = BT / 4, KPI = 64 / CPK;
+        const int kk = ins * KPI + l / CPK;
+        const int c = (l % CPK) ^ swz_k<RBK>(kk);
+        const i64 col = R0 + 4 * c <= rows - 4 ? 4 * c : rows - 4 - R0;
+        return col + kk * ld;
+    }
+}
+
+template <int BT, bool BUF, bool KC>
+__device__ __forceinline__ void piece(const float* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int ins,
+                                      lds_char* img) {
+    const float* base = KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
+    if constexpr (BUF) {
+        const BufferSrc<float> src(base, (KC ? BT : G<BT>::RBK) * ld * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + ins * 1024),
+                                                 16, off, 0, 0, 0);
+    } else {
+        __builtin_amdgcn_global_load_lds((const void*)(base + goff),
+                                         (__attribute__((address_space(3))) void*)(img + ins * 1024), 16, 0, 0);
+    }
+}
+
+// quad j's four values of one 16-row fragment: v[e] = X(R0 + (l&15), KS (l>>4) + 4 j + e)
+template <int BT, bool KC>
+__device__ __forceinline__ void quad(const lds_char* img, int R0, int j, int l, float (&v)[4]) {
+    constexpr int RBK = G<BT>::RBK, KS = G<BT>::KS;
+    const int r = R0 + (l & 15), g = l >> 4;
+    if (KC) {
+        const int c = (KS / 4) * g + j;
+        const f32x4 x = *(const __attribute__((address_space(3))) f32x4*)(img + r * (RBK * 4) + ((c ^ swz_r(r)) << 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = x[e];
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int kk = KS * g + 4 * j + e;
+            const int off = kk * (BT * 4) + (((r >> 2) ^ swz_k<RBK>(kk)) << 4) + ((r & 3) << 2);
+            v[e] = *(const __attribute__((address_space(3))) float*)(img + off);
+        }
+    }
+}
+
+template <int BT>
+struct Ops { float a[G<BT>::MI][4], b[G<BT>::MI][4]; };
+struct Pieces { int offA[8], offB[8]; i64 gA[8], gB[8]; };
+
+// one quad: the MFMAs of four k-steps on `cur`; quad `jrd` of rdA / rdB into
+// `nxt` over the first half of them (fragment f after MFMA f MI); NP pieces u0..
+// of one unit into `st` over the second half (SB: of B, else of A).  Unrolled
+// by a fold over the MFMA index, not a loop: the placement is then constexpr.
+template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
+struct Quad {
+    static constexpr int MI = G<BT>::MI, NM = G<BT>::NM, NR = G<BT>::NR, WT = G<BT>::WT, H = NM / 2;
+    const FParams& p;
+    i64 m0, n0;
+    int w, l, wr, wc;
+    const Pieces& pc;
+    const lds_char* __restrict__ rdA;
+    const lds_char* __restrict__ rdB;
+    int jrd;
+    lds_char* __restrict__ st;
+    int u0;
+    i64 k0;
+
+    template <int I>
+    __device__ __forceinline__ void step(f32x4 (&acc)[MI][MI], const Ops<BT>& cur, Ops<BT>& nxt) const {
+        constexpr int e = I / (MI * MI), mi = (I / MI) % MI, ni = I % MI;
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.a[mi][e], cur.b[ni][e], acc[mi][ni], 0, 0, 0);
+        if constexpr (I % MI == 0 && I / MI < NR) {
+            constexpr int f = I / MI;
+            if constexpr (f < MI) quad<BT, KCA>(rdA, wr * WT + f * 16, jrd, l, nxt.a[f]);
+            else quad<BT, KCB>(rdB, wc * WT + (f - MI) * 16, jrd, l, nxt.b[f - MI]);
+        }
+        if constexpr (NP > 0 && I >= H && (I - H) % (H / NP) == 0) {
+            const int u = u0 + (I - H) / (H / NP);
+            if constexpr (SB) piece<BT, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+            else piece<BT, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the placement as written
+    }
+    template <int... Is>
+    __device__ __forceinline__ void run(f32x4 (&acc)[MI][MI], const Ops<BT>& cur, Ops<BT>& nxt,
+                                        std::integer_sequence<int, Is...>) const {
+        (step<Is>(acc, cur, nxt), ...);
+    }
+};
+
+template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
+__device__ __forceinline__ void qstep(const FParams& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
+                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const lds_char* __restrict__ rdB, int jrd, lds_char* __restrict__ st, int u0,
+                                      i64 k0, f32x4 (&acc)[G<BT>::MI][G<BT>::MI], const Ops<BT>& cur, Ops<BT>& nxt) {
+    const Quad<BT, KCA, KCB, BUF, SB, NP> q{p, m0, n0, w, l, wr, wc, pc, rdA, rdB, jrd, st, u0, k0};
+    q.run(acc, cur, nxt, std::make_integer_sequence<int, G<BT>::NM>{});
+}
+}  // namespace fring
+
+template <int BT, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
+    using namespace fring;
+    constexpr int RBK = G<BT>::RBK, WT = G<BT>::WT, MI = G<BT>::MI, NQ = G<BT>::NQ, PPQ = 16 / NQ;
+    __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
+    lds_char* lds = (lds_char*)lds_raw;
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const i64 m0 = (i64)tm * BT, n0 = (i64)tn * BT;
+    {
+        const i64 kz0 = (i64)blockIdx.y * p.kchunk;
+        p.k = min(p.kchunk, p.k - kz0);
+        p.A += KCA ? kz0 : kz0 * p.lda;
+        p.B += KCB ? kz0 : kz0 * p.ldb;
+        p.C += (i64)blockIdx.y * p.zstride;
+    }
+    Pieces pc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        pc.gA[u] = piece_off<BT, KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<BT, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.offA[u] = (int)(pc.gA[u] * 4);
+        pc.offB[u] = (int)(pc.gB[u] * 4);
+    }
+    f32x4 acc[MI][MI];
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MI; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+    const int nt = (int)(p.k / RBK);
+    auto kt = [&](int t) { return (i64)min(t, nt - 1) * RBK; };
+    // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; quad (0,0)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            piece<BT, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            piece<BT, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+    }
+    wait_cnt<16, NOWAIT_LGKM>();
+    dma_barrier();
+    Ops<BT> X, Y;
+#pragma unroll
+    for (int f = 0; f < MI; ++f) {
+        quad<BT, KCA>(lds, wr * WT + f * 16, 0, l, X.a[f]);
+        quad<BT, KCB>(lds + UNIT, wc * WT + f * 16, 0, l, X.b[f]);
+    }
+    wait_cnt<NOWAIT_VM, 0>();
+    auto ktile = [&](auto jc, int t) {
+        constexpr int J = decltype(jc)::value;
+        constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
+                      sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
+        const lds_char* rA = lds + sA * UNIT;
+        const lds_char* rB = lds + sB * UNIT;
+        const i64 k2 = kt(t + 2);
+        // quads 0..NQ-2 (operands alternate X -> Y -> X; NQ is even); A_{t+2} over the first half
+        auto q = [&](auto qc) {
+            constexpr int Q = decltype(qc)::value;
+            constexpr int NP = Q < NQ / 2 ? PPQ : 0;
+            if constexpr (Q % 2 == 0)
+                qstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
+                                                    Q * PPQ, k2, acc, X, Y);
+            else
+                qstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
+                                                    Q * PPQ, k2, acc, Y, X);
+            if constexpr (Q < NQ - 2) wait_cnt<NOWAIT_VM, 0>();
+        };
+        q(std::integral_constant<int, 0>{});
+        q(std::integral_constant<int, 1>{});
+        q(std::integral_constant<int, 2>{});
+        if constexpr (NQ == 8) {
+            q(std::integral_constant<int, 3>{});
+            q(std::integral_constant<int, 4>{});
+            q(std::integral_constant<int, 5>{});
+            q(std::integral_constant<int, 6>{});
+        }
+        wait_cnt<8, 0>();
+        dma_barrier();
+        // quad NQ-1: quad (t+1, 0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
+        qstep<BT, KCA, KCB, BUF, true, 8>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+                                          lds + st1 * UNIT, 0, k2, acc, Y, X);
+        wait_cnt<NOWAIT_VM, 0>();
+    };
+    for (int t = 0; t < nt; t += NSLOT) {
+        ktile(std::integral_constant<int, 0>{}, t);
+        if (t + 1 < nt) ktile(std::integral_constant<int, 1>{}, t + 1);
+        if (t + 2 < nt) ktile(std::integral_constant<int, 2>{}, t + 2);
+        if (t + 3 < nt) ktile(std::integral_constant<int, 3>{}, t + 3);
+        if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
+
+    // Epilogue: C/D map of v_mfma_f32_16x16x4_f32: row = 4*(lane>>4) + reg, col = lane&15
+    const int g = l >> 4, c = l & 15;
+    const i64 ib = m0 + wr * WT + 4 * g, jb = n0 + wc * WT + c;
+    if (p.vec_c && m0 + BT <= p.m && n0 + BT <= p.n) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+            f32x4 cv[MI];
+            if (!BETA0) {
+#pragma unroll
+                for (int ni = 0; ni < MI; ++ni)
+                    cv[ni] = *reinterpret_cast<const f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16);
+            }
+#pragma unroll
+            for (int ni = 0; ni < MI; ++ni) {
+                f32x4 v = p.alpha * acc[mi][ni];
+                if (!BETA0) v += p.beta * cv[ni];
+                *reinterpret_cast<f32x4*>(p.C + (jb + ni * 16) * p.ldc + ib + mi * 16) = v;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MI; ++ni) {
+            const i64 j = jb + ni * 16;
+            if (j >= p.n) continue;
+            float* col = p.C + j * p.ldc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const i64 i = ib + mi * 16 + r;
+                if (i < p.m) {
+                    const float v = p.alpha * acc[mi][ni][r];
+                    col[i] = BETA0 ? v : v + p.beta * col[i];
+                }
+            }
+        }
+}
+
+template <int BT, bool KCA, bool KCB>
+hipError_t launch_fr(FParams p, hipStream_t s) {
+    constexpr int RBK = fring::G<BT>::RBK;
+    p.tiles_m = (int)((p.m + BT - 1) / BT);
+    p.tiles_n = (int)((p.n + BT - 1) / BT);
+    const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
+    const bool buf = dma_fits(KCA ? BT : RBK, p.lda, 4) && dma_fits(KCB ? BT : RBK, p.ldb, 4);
+    if (p.beta == 0.f) {
+        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
+    } else {
+        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
 template <typename SH, bool KCA, bool KCB, bool BUF>
 hipError_t launch_fw(FParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + SH::BM - 1) / SH::BM);
@@ -278,6 +577,28 @@ bool t64_tiles(i64 m, i64 n) {
     return prefer_t64(v, m, n);
 }
 
+// the ring kernel's tile edge for this grid (0: the slab kernels).  Measured
+// against the slab kernels in one process (profiles/r05t_f32_ring_ab.log):
+//  * 64 x 64 ring on grids of at most 256 64-tiles (one round of workgroups):
+//    1024^2 x 2048 NN / TN / NT / TT 95 / 100 / 94 / 95 -> 116 / 124 / 112 /
+//    116 TF; with more (1536 x 2048^2, three per CU in turn) 129 -> 120: slab;
+//  * 128 x 128 ring where both operands are k-contiguous (TN): 16384^3 150.0 ->
+//    151.8, 8192^2 x 65536 (C4's shape) 149.9 -> 152.3, 2048^3 132.8 -> 140.8;
+//    with a rows-contiguous operand (its fragments four ds_read_b32 per quad)
+//    it loses (16384^3 NN 150.7 -> 145.3, NT 149.6 -> 139.5): slab.
+// ELX_F32G_RING (read per call, for the A/B and the tests) overrides: bit 0 the
+// 128 x 128 ring on every grid of 128-tiles, bit 1 the 64 x 64 ring on every
+// grid of 64-tiles, 0 neither.
+int ring_bt(bool kca, bool kcb, i64 m, i64 n) {
+    const char* e = getenv("ELX_F32G_RING");
+    if (t64_tiles(m, n)) {
+        if (e) return (atoi(e) & 2) ? 64 : 0;
+        return (m + 63) / 64 * ((n + 63) / 64) <= 256 ? 64 : 0;
+    }
+    if (e) return (atoi(e) & 1) ? 128 : 0;
+    return kca && kcb ? 128 : 0;
+}
+
 template <bool KCA, bool KCB, bool BUF>
 hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // 64 x 64 wave tiles (the fp64 kernel's choice) measured a wash on square
@@ -288,6 +609,9 @@ hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // profiles/r03_f32_wtm.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
+    const int bt = ring_bt(KCA, KCB, p.m, p.n);
+    if (bt == 128 && p.k % 64 == 0 && p.kchunk % 64 == 0) return launch_fr<128, KCA, KCB>(p, s);
+    if (bt == 64 && p.k % 128 == 0 && p.kchunk % 128 == 0) return launch_fr<64, KCA, KCB>(p, s);
     if (t64_tiles(p.m, p.n)) {
         // at most one workgroup per CU: a 4-slab LDS ring unless NN (NT 1024^2 x
         // 2048 72.7 -> 93.7 TF, TN 96.4 -> 99.8, NN even; the fp64 kernel lost
@@ -317,6 +641,11 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 4 == 0 && ldb % 4 == 0 && (kca || (m % 4 == 0 && m >= 4)) &&
                     (kcb || (n % 4 == 0 && n >= 4)) && m < (1ll << 31) && n < (1ll << 31);
+    const int bt = ring_bt(kca, kcb, m, n);
+    if (bt) {  // one workgroup per CU, K-tiles of 8192 / bt
+        const int rbk = 8192 / bt;
+        return dma_plan(ok && k >= rbk, (m + bt - 1) / bt * ((n + bt - 1) / bt), k, rbk, 256);
+    }
     if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }

@@ -551,7 +551,7 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
                     (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
     if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
-    if (ring_tiles(m, n)) return dma_plan(ok && k >= ring::RBK, (m + 127) / 128 * ((n + 127) / 128), k, ring::RBK);
+    if (ring_tiles(m, n)) return dma_plan(ok && k >= ring::RBK, (m + 127) / 128 * ((n + 127) / 128), k, ring::RBK, 256);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 

@@ -28,11 +28,13 @@ struct DmaPlan {
     i64 kmain, kchunk;
     int nz;
 };
-inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk) {
+// slots: workgroups the chip holds at once (512: two per CU; the fp64 ring
+// kernel's one per CU: 256, so its 2048^2 x 16384 runs whole-k, 256 tiles, with
+// no partials' round trip)
+inline DmaPlan dma_plan(bool ok, i64 tiles, i64 k, int bk, i64 slots = 512) {
     DmaPlan d{false, 0, 0, 1};
     if (!ok) return d;
     d.kmain = k / bk * bk;
-    const i64 slots = 512;  // two workgroups per CU
     if (tiles >= slots) {
         d.use = true;
         d.kchunk = d.kmain;

@@ -189,6 +189,44 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     assert np.array_equal(got, want), f"{int(np.count_nonzero(got != want))} mismatches"
 
 
+@pytest.mark.parametrize("ta", ["N", "T"])
+@pytest.mark.parametrize("tb", ["N", "T"])
+@pytest.mark.parametrize("ring,shape,beta", [
+    ("1", (2048, 2048, 640), -1.0), ("1", (4000, 4040, 1088), 0.0), ("1", (2048, 4096, 2072), -1.0),
+    ("1", (4096, 2048, 64), 0.5),
+    ("2", (1024, 1024, 2048), -1.0), ("2", (1000, 1016, 1152), 0.0), ("2", (1536, 2048, 2100), -1.0),
+    ("2", (1024, 512, 128), 0.5),
+    ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)])
+def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
+    """The fp32 ring kernel (gemm_f32r_kernel; ELX_F32G_RING bit 0: 128 x 128
+    tiles with 64-deep K-tiles on grids of 128-tiles, bit 1: 64 x 64 tiles with
+    128-deep K-tiles on grids of 64-tiles): many wraps of the 5-slot ring, ragged
+    edge tiles with beta = 0 (C holds NaN and must not be read), the k tail
+    through the general kernel (2072 = 32 x 64 + 24, 2100 = 16 x 128 + 52), a
+    single K-tile (prologue and clamped restaging only), and the k-permuted
+    MFMA steps in every orientation.  ring = "0": the slab kernels on the ragged
+    cases.  Integer operands: exact."""
+    monkeypatch.setenv("ELX_F32G_RING", ring)
+    m, n, k = shape
+    rng = np.random.default_rng(m + k + 1)
+    A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float32))
+    B = np.asfortranarray(rng.integers(-4, 4, (k, n) if tb == "N" else (n, k)).astype(np.float32))
+    C = np.asfortranarray(rng.integers(-4, 4, (m, n)).astype(np.float32))
+    C0 = C.copy()
+    if beta == 0.0:
+        C0[:] = np.nan
+    dA, dB, dC = dev(A), dev(B), dev(C0)
+    torch.cuda.synchronize()
+    L.call("elx_gemm_f32", OPS[ta], OPS[tb], m, n, k, 2.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0],
+           beta, dC.data_ptr(), m, None)
+    sync()
+    opA = (A if ta == "N" else A.T).astype(np.float64)
+    opB = (B if tb == "N" else B.T).astype(np.float64)
+    want = (2.0 * (opA @ opB) + (beta * C if beta != 0.0 else 0.0)).astype(np.float32)
+    got = host(dC, (m, n), np.float32)
+    assert np.array_equal(got, want), f"{int(np.count_nonzero(got != want))} mismatches"
+
+
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])

@@ -4,7 +4,8 @@
 
 Random Uniform(-0.5, 0.5) operands (column-major), beta = 1; each timing is the best
 of 3 runs of back-to-back calls (launch latency amortised).  --vendor also
-times torch.matmul (hipBLASLt) on the same shape as a reference point.
+times torch.matmul (hipBLASLt) on the same shape as a reference point, and ours
+at beta = 0 beside it (the vendor call's C = op(A) op(B) reads no C).
 """
 import os
 import sys
@@ -59,6 +60,11 @@ def run(dt, ta, tb, m, n, k, vendor, reps=3):
     t = timeit(go, reps)
     line = f"{dt} {'T' if ta else 'N'}{'T' if tb else 'N'} {m}x{n}x{k}: {2*m*n*k/t/1e12:8.2f} TFLOP/s ({t*1e3:.2f} ms)"
     if vendor:
+        # torch.matmul(out=) is C = op(A) op(B), beta = 0 (no C read): ours likewise beside it
+        go0 = lambda: L.check(fn(ta, tb, m, n, k, 1.0, A.data_ptr(), lda, B.data_ptr(), ldb, 0.0, C.data_ptr(), m,
+                                 None))
+        t0 = timeit(go0, reps)
+        line += f"   beta=0 {2*m*n*k/t0/1e12:8.2f}"
         # same column-major problem through torch (row-major views): C^T = op(B)^T op(A)^T
         At = A.view(m if ta else k, lda)  # row-major view of column-major A: At[c, r] = A(r, c)
         Bt = B.view(k if tb else n, ldb)

@@ -5,7 +5,7 @@ correction in MI355X_MICROARCH.md §HBM, + WRITE_SIZE; both in KB)."""
 import csv, glob, json, os, shutil, sys
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 key = sys.argv[2] if len(sys.argv) > 2 else "f64:32768:1"  # dtype:n:n_gpus of the profiled bench command
-kpat = sys.argv[3] if len(sys.argv) > 3 else "gemm_f64g_kernel"  # the dominant kernel's name fragment
+kpat = sys.argv[3] if len(sys.argv) > 3 else "gemm_f64r_kernel"  # the dominant kernel's name fragment
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "gpurun_out")
 prof = os.path.join(root, "profiles")
