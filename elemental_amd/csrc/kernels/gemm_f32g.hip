@@ -296,20 +296,26 @@ __device__ __forceinline__ int swz_r(int r) { return r & 15; }
 template <int RBK>
 __device__ __forceinline__ int swz_k(int kk) { return ((kk / (RBK / 4)) & 3) << 2; }
 
+// RC images in 256-B lines: a 1-KiB piece = four consecutive k-rows x one
+// 256-B line of the k-row (NSEG lines per k-row).  Two whole 512-B k-rows per
+// piece (BT 128) measured 3.5-6 % slower, as in the fp64 ring
+// (profiles/r05ab_f32_lines_ab.log, r05aa_f64_rcblk_ab.log).
 // per-lane element offset of piece `ins` (0..31) of one operand's K-tile image
 template <int BT, bool KC>
 __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
-    constexpr int RBK = G<BT>::RBK;
-    if (KC) {  // rows of RBK floats; RPI rows per 1-KiB piece
+    constexpr int RBK = G<BT>::RBK, KS = G<BT>::KS;
+    if (KC) {  // whole rows of RBK floats, RPI rows per piece (the 256-B lines of
+               // 512-B rows measured slower at BT 64: TN 1024^2 x 2048 124 -> 120 TF)
         constexpr int CPR = RBK / 4, RPI = 64 / CPR;
         const int r = ins * RPI + l / CPR;
         const int c = (l % CPR) ^ swz_r(r);
         const i64 row = R0 + r < rows ? r : rows - 1 - R0;
         return row * ld + 4 * c;
-    } else {   // k-rows of BT floats; KPI k-rows per piece
-        constexpr int CPK = BT / 4, KPI = 64 / CPK;
-        const int kk = ins * KPI + l / CPK;
-        const int c = (l % CPK) ^ swz_k<RBK>(kk);
+    } else {   // k-rows 4 kq.. of BT floats, line ins % NSEG; chunk ^ 4 g(kq)
+        constexpr int NSEG = BT * 4 / 256;
+        const int kq = ins / NSEG;
+        const int kk = kq * 4 + (l >> 4);
+        const int c = (ins % NSEG) * 16 + ((l & 15) ^ (((kq / (KS / 4)) & 3) << 2));
         const i64 col = R0 + 4 * c <= rows - 4 ? 4 * c : rows - 4 - R0;
         return col + kk * ld;
     }
@@ -340,10 +346,12 @@ __device__ __forceinline__ void quad(const lds_char* img, int R0, int j, int l, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = x[e];
     } else {
+        constexpr int NSEG = BT * 4 / 256;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int kk = KS * g + 4 * j + e;
-            const int off = kk * (BT * 4) + (((r >> 2) ^ swz_k<RBK>(kk)) << 4) + ((r & 3) << 2);
+            const int kq = (KS / 4) * g + j;  // k = 4 kq + e
+            const int off = (kq * NSEG + (r >> 6)) * 1024 + e * 256 +
+                            ((((r & 63) >> 2) ^ (((kq / (KS / 4)) & 3) << 2)) << 4) + ((r & 3) << 2);
             v[e] = *(const __attribute__((address_space(3))) float*)(img + off);
         }
     }
@@ -578,14 +586,16 @@ bool t64_tiles(i64 m, i64 n) {
 }
 
 // the ring kernel's tile edge for this grid (0: the slab kernels).  Measured
-// against the slab kernels in one process (profiles/r05t_f32_ring_ab.log):
+// against the slab kernels in one process (profiles/r05t_f32_ring_ab.log, and
+// with the RC images in 256-B lines profiles/r05ac_f32_ring_policy_ab.log):
 //  * 64 x 64 ring on grids of at most 256 64-tiles (one round of workgroups):
-//    1024^2 x 2048 NN / TN / NT / TT 95 / 100 / 94 / 95 -> 116 / 124 / 112 /
-//    116 TF; with more (1536 x 2048^2, three per CU in turn) 129 -> 120: slab;
-//  * 128 x 128 ring where both operands are k-contiguous (TN): 16384^3 150.0 ->
-//    151.8, 8192^2 x 65536 (C4's shape) 149.9 -> 152.3, 2048^3 132.8 -> 140.8;
-//    with a rows-contiguous operand (its fragments four ds_read_b32 per quad)
-//    it loses (16384^3 NN 150.7 -> 145.3, NT 149.6 -> 139.5): slab.
+//    1024^2 x 2048 NN / TN / NT / TT 95 / 100 / 94 / 95 -> 123 / 124 / 123 / 122
+//    TF; with more (1536 x 2048^2, three per CU in turn) 128 -> 120-126: slab;
+//  * 128 x 128 ring where A is k-contiguous (TN, TT): 16384^3 TN 150.0 -> 151,
+//    TT 148.5 -> 149.5, 8192^2 x 65536 (C4's shape) 149.4 -> 151.6, 4096^3 TT
+//    145.3 -> 146.2; with A rows-contiguous (NN, NT) the slab kernel's two
+//    workgroups per CU stay ahead below 16384^3 (C3-f32's 65536 x 8192^2 panel
+//    150.1 vs 147.6, 8192^3 149.8 vs 147.4, 4096^3 NN 146.9 vs 145.4).
 // ELX_F32G_RING (read per call, for the A/B and the tests) overrides: bit 0 the
 // 128 x 128 ring on every grid of 128-tiles, bit 1 the 64 x 64 ring on every
 // grid of 64-tiles, 0 neither.
@@ -596,7 +606,7 @@ int ring_bt(bool kca, bool kcb, i64 m, i64 n) {
         return (m + 63) / 64 * ((n + 63) / 64) <= 256 ? 64 : 0;
     }
     if (e) return (atoi(e) & 1) ? 128 : 0;
-    return kca && kcb ? 128 : 0;
+    return kca ? 128 : 0;
 }
 
 template <bool KCA, bool KCB, bool BUF>

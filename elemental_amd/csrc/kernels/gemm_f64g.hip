@@ -281,12 +281,25 @@ __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 l
         const int c = (l & 15) ^ swz_kc<RBK>(r);
         const i64 row = R0 + r < rows ? r : rows - 1 - R0;
         return row * ld + 2 * c;
-    } else {   // one 1-KiB k-row per piece; chunk c at c ^ 8 (kk & 1)
-        const int kk = ins;
-        const int c = l ^ ((kk & 1) << 3);
-        const i64 col = R0 + 2 * c <= rows - 2 ? 2 * c : rows - 2 - R0;
+    } else {   // blocked: piece = 4 k-rows 4 (ins>>2).. x one 256-B quarter (ins & 3) of the
+               // 128 rows; chunk c at c ^ 8 (kk & 1).  One 1-KiB k-row per piece instead
+               // (the slab kernel's shape) ran NN / NT / TT 2.5 / 5.4 / 2.8 % slower at
+               // 16384^3, 2048^3 NN 69.4 -> 70.9 TF (profiles/r05aa_f64_rcblk_ab.log)
+        const int kk = (ins >> 2) * 4 + (l >> 4);
+        const int c = (l & 15) ^ ((kk & 1) << 3);
+        const int col0 = (ins & 3) * 32 + 2 * c;
+        const i64 col = R0 + col0 <= rows - 2 ? col0 : rows - 2 - R0;
         return col + kk * ld;
     }
+}
+// operand of k-step s for rows R0..R0+15 from a ring image (KC: opnd's layout;
+// RC: the blocked layout above, 1-KiB block (s, r>>5), sub-row k & 3)
+template <bool KC>
+__device__ __forceinline__ double ropnd(const lds_char* img, int R0, int s, int l) {
+    if (KC) return opnd<true, 128, RBK>(img, R0, s, l);
+    const int r = R0 + (l & 15), g = l >> 4;
+    const int off = (s * 4 + (r >> 5)) * 1024 + g * 256 + ((((r & 31) >> 1) ^ ((g & 1) << 3)) << 4) + ((r & 1) << 3);
+    return *(const __attribute__((address_space(3))) double*)(img + off);
 }
 
 template <bool BUF, bool KC>
@@ -329,8 +342,8 @@ __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, i
     for (int i = 0; i < 16; ++i) {
         mfma_acc(acc[i >> 2][i & 3], cur.a[i >> 2], cur.b[i & 3]);
         if (i < 8) {  // the next k-step's operands, one read per MFMA
-            if (i < 4) nxt.a[i] = opnd<KCA, 128, RBK>(rdA, wr * WT + i * 16, srd, l);
-            else nxt.b[i - 4] = opnd<KCB, 128, RBK>(rdB, wc * WT + (i - 4) * 16, srd, l);
+            if (i < 4) nxt.a[i] = ropnd<KCA>(rdA, wr * WT + i * 16, srd, l);
+            else nxt.b[i - 4] = ropnd<KCB>(rdB, wc * WT + (i - 4) * 16, srd, l);
         }
         if constexpr (NP > 0) {
             if (i >= 8 + OFF && (i - 8 - OFF) % SP == 0 && (i - 8 - OFF) / SP < NP) {
@@ -392,8 +405,8 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
     Ops X, Y;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        X.a[q] = opnd<KCA, 128, RBK>(lds, wr * WT + q * 16, 0, l);
-        X.b[q] = opnd<KCB, 128, RBK>(lds + UNIT, wc * WT + q * 16, 0, l);
+        X.a[q] = ropnd<KCA>(lds, wr * WT + q * 16, 0, l);
+        X.b[q] = ropnd<KCB>(lds + UNIT, wc * WT + q * 16, 0, l);
     }
     wait_cnt<NOWAIT_VM, 0>();
     auto ktile = [&](auto jc, int t) {
