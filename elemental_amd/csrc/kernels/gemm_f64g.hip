@@ -35,6 +35,7 @@ namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 16, GROUP_M = 8;
+constexpr bool RING64_DEFAULT = true;  // the 64 x 64 ring on grids of 64-tiles by default
 // Tile shape: BM = 128 rows, slab depth SK = 16 (two 32-KiB stages: two
 // workgroups per CU); wave tiles WTM x 64 with WTM = 32 (2 x 4 accumulators,
 // 0.75 ds_read per MFMA) or 64 (4 x 4 accumulators, 0.5 ds_read per MFMA, half
@@ -271,43 +272,59 @@ __global__ __launch_bounds__(SH::NT, SH::WAVES_PER_EU) void gemm_f64g_kernel(GPa
 // of DMA lead.
 // ---------------------------------------------------------------------------
 namespace ring {
-constexpr int RBK = 32, NSLOT = 5, UNIT = 128 * RBK * 8, WT = 64;
+constexpr int NSLOT = 5;
+// BT 128: the kernel above.  BT 64 (round 5, grids of 64-tiles): four waves of
+// 32 x 32 (2 x 2 accumulators), K-tiles of 16 k (8 KiB per image, 40 KiB of
+// ring), four workgroups per CU, 4 k-steps of 4 MFMAs per K-tile; the same
+// schedule with 2 pieces per wave and image.
+template <int BT>
+struct RG {
+    static constexpr int RBK = BT == 128 ? 32 : 16, UNIT = BT * RBK * 8, WT = BT / 2, MI = WT / 16;
+    static constexpr int NKS = RBK / 4;                // k-steps per K-tile
+    static constexpr int NPW = UNIT / 1024 / 4;        // pieces per wave and image
+    static constexpr int NM = MI * MI, NR = 2 * MI;    // MFMAs and operand reads per k-step
+    static constexpr int MINB = BT == 128 ? 1 : 4;     // workgroups per CU
+};
 
-// per-lane element offset of piece `ins` (0..31) of one operand's K-tile image
-template <bool KC>
+// per-lane element offset of piece `ins` of one operand's K-tile image
+template <int BT, bool KC>
 __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
-    if (KC) {  // 4 rows of 256 B per piece; chunk c of row r at c ^ (r & 15)
-        const int r = ins * 4 + (l >> 4);
-        const int c = (l & 15) ^ swz_kc<RBK>(r);
+    constexpr int RBK = RG<BT>::RBK;
+    if (KC) {  // RPI rows of RBK doubles per piece; chunk c of row r at c ^ swz_kc(r)
+        constexpr int CPR = RBK / 2, RPI = 64 / CPR;
+        const int r = ins * RPI + l / CPR;
+        const int c = (l % CPR) ^ swz_kc<RBK>(r);
         const i64 row = R0 + r < rows ? r : rows - 1 - R0;
         return row * ld + 2 * c;
-    } else {   // blocked: piece = 4 k-rows 4 (ins>>2).. x one 256-B quarter (ins & 3) of the
-               // 128 rows; chunk c at c ^ 8 (kk & 1).  One 1-KiB k-row per piece instead
+    } else {   // blocked: piece = 4 k-rows 4 (ins / NSEG).. x one 256-B line (ins % NSEG)
+               // of the BT rows; chunk c at c ^ 8 (kk & 1).  One 1-KiB k-row per piece instead
                // (the slab kernel's shape) ran NN / NT / TT 2.5 / 5.4 / 2.8 % slower at
                // 16384^3, 2048^3 NN 69.4 -> 70.9 TF (profiles/r05aa_f64_rcblk_ab.log)
-        const int kk = (ins >> 2) * 4 + (l >> 4);
+        constexpr int NSEG = BT * 8 / 256;
+        const int kk = (ins / NSEG) * 4 + (l >> 4);
         const int c = (l & 15) ^ ((kk & 1) << 3);
-        const int col0 = (ins & 3) * 32 + 2 * c;
+        const int col0 = (ins % NSEG) * 32 + 2 * c;
         const i64 col = R0 + col0 <= rows - 2 ? col0 : rows - 2 - R0;
         return col + kk * ld;
     }
 }
 // operand of k-step s for rows R0..R0+15 from a ring image (KC: opnd's layout;
 // RC: the blocked layout above, 1-KiB block (s, r>>5), sub-row k & 3)
-template <bool KC>
+template <int BT, bool KC>
 __device__ __forceinline__ double ropnd(const lds_char* img, int R0, int s, int l) {
-    if (KC) return opnd<true, 128, RBK>(img, R0, s, l);
+    if (KC) return opnd<true, BT, RG<BT>::RBK>(img, R0, s, l);
+    constexpr int NSEG = BT * 8 / 256;
     const int r = R0 + (l & 15), g = l >> 4;
-    const int off = (s * 4 + (r >> 5)) * 1024 + g * 256 + ((((r & 31) >> 1) ^ ((g & 1) << 3)) << 4) + ((r & 1) << 3);
+    const int off = (s * NSEG + (r >> 5)) * 1024 + g * 256 + ((((r & 31) >> 1) ^ ((g & 1) << 3)) << 4) + ((r & 1) << 3);
     return *(const __attribute__((address_space(3))) double*)(img + off);
 }
 
-template <bool BUF, bool KC>
+template <int BT, bool BUF, bool KC>
 __device__ __forceinline__ void piece(const double* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int ins,
                                       lds_char* img) {
     const double* base = KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
     if constexpr (BUF) {
-        const BufferSrc<double> src(base, (KC ? 128 : RBK) * ld * 8);
+        const BufferSrc<double> src(base, (KC ? BT : RG<BT>::RBK) * ld * 8);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + ins * 1024),
                                                  16, off, 0, 0, 0);
     } else {
@@ -316,9 +333,11 @@ __device__ __forceinline__ void piece(const double* X, i64 ld, i64 R0, i64 k0, i
     }
 }
 
-struct Ops { double a[4], b[4]; };
-// this lane's buffer offsets (bytes) / element offsets of its 8 pieces per operand
-struct Pieces { int offA[8], offB[8]; i64 gA[8], gB[8]; };
+template <int BT>
+struct Ops { double a[RG<BT>::MI], b[RG<BT>::MI]; };
+// this lane's buffer offsets (bytes) / element offsets of its pieces per operand
+template <int BT>
+struct Pieces { int offA[RG<BT>::NPW], offB[RG<BT>::NPW]; i64 gA[RG<BT>::NPW], gB[RG<BT>::NPW]; };
 
 // acc += a b.  The builtin, not asm: hipcc's hazard recognizer then pads the
 // operand hazards (an asm MFMA here gave wrong products on 1.4 % of the entries:
@@ -329,27 +348,36 @@ __device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
 }
 
-// one k-step: 16 MFMAs on `cur`, the next k-step's operands (k-step `srd` of the
-// K-tile in rdA / rdB) into `nxt`, and NP pieces u0.. of one unit into `st`
-template <bool KCA, bool KCB, bool BUF, bool SB, int NP>
+// one k-step: NM MFMAs on `cur`; the next k-step's NR operand reads (k-step
+// `srd` of the K-tile in rdA / rdB) into `nxt` over the first half of them; NP
+// pieces u0.. of one unit into `st` over the second half
+template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
 __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
-                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const Pieces<BT>& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st,
-                                      int u0, i64 k0, f64x4 (&acc)[4][4], const Ops& cur, Ops& nxt) {
-    // pieces in the second half of the MFMAs, SP apart (reads in the first half)
-    constexpr int SP = NP > 0 ? 8 / NP : 1, OFF = SP > 1 ? 1 : 0;
+                                      int u0, i64 k0, f64x4 (&acc)[RG<BT>::MI][RG<BT>::MI], const Ops<BT>& cur,
+                                      Ops<BT>& nxt) {
+    constexpr int MI = RG<BT>::MI, NM = RG<BT>::NM, NR = RG<BT>::NR, WT = RG<BT>::WT, H = NM / 2;
+    // BT 128: reads one per MFMA of the first half, pieces SP apart in the second
+    // half from its second MFMA on (at 2 pieces); BT 64: two reads per MFMA
+    constexpr int RPM = NR / H;
+    constexpr int SP = NP > 0 ? H / NP : 1, OFF = (SP > 1 && BT == 128) ? 1 : 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        mfma_acc(acc[i >> 2][i & 3], cur.a[i >> 2], cur.b[i & 3]);
-        if (i < 8) {  // the next k-step's operands, one read per MFMA
-            if (i < 4) nxt.a[i] = ropnd<KCA>(rdA, wr * WT + i * 16, srd, l);
-            else nxt.b[i - 4] = ropnd<KCB>(rdB, wc * WT + (i - 4) * 16, srd, l);
+    for (int i = 0; i < NM; ++i) {
+        mfma_acc(acc[i / MI][i % MI], cur.a[i / MI], cur.b[i % MI]);
+        if (i < H) {
+#pragma unroll
+            for (int q = 0; q < RPM; ++q) {
+                const int f = i * RPM + q;
+                if (f < MI) nxt.a[f] = ropnd<BT, KCA>(rdA, wr * WT + f * 16, srd, l);
+                else nxt.b[f - MI] = ropnd<BT, KCB>(rdB, wc * WT + (f - MI) * 16, srd, l);
+            }
         }
         if constexpr (NP > 0) {
-            if (i >= 8 + OFF && (i - 8 - OFF) % SP == 0 && (i - 8 - OFF) / SP < NP) {
-                const int u = u0 + (i - 8 - OFF) / SP;
-                if constexpr (SB) piece<BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-                else piece<BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+            if (i >= H + OFF && (i - H - OFF) % SP == 0 && (i - H - OFF) / SP < NP) {
+                const int u = u0 + (i - H - OFF) / SP;
+                if constexpr (SB) piece<BT, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BT, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
             }
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the placement as written
@@ -357,9 +385,12 @@ __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, i
 }
 }  // namespace ring
 
-template <bool KCA, bool KCB, bool BETA0, bool BUF>
-__global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
+template <int BT, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GParams p) {
     using namespace ring;
+    using G = RG<BT>;
+    constexpr int RBK = G::RBK, UNIT = G::UNIT, WT = G::WT, MI = G::MI, NKS = G::NKS, NPW = G::NPW;
+    constexpr int NPA = NPW / (NKS / 2);  // pieces of A_{t+2} per k-step over the first half
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
@@ -367,7 +398,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
     const int wr = w >> 1, wc = w & 1;
     int tm, tn;
     tile_of(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, p.group_m, p.xcd_remap, tm, tn);
-    const i64 m0 = (i64)tm * 128, n0 = (i64)tn * 128;
+    const i64 m0 = (i64)tm * BT, n0 = (i64)tn * BT;
     {
         const i64 kz0 = (i64)blockIdx.y * p.kchunk;
         p.k = min(p.kchunk, p.k - kz0);
@@ -375,19 +406,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
         p.B += KCB ? kz0 : kz0 * p.ldb;
         p.C += (i64)blockIdx.y * p.zstride;
     }
-    Pieces pc;
+    Pieces<BT> pc;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
-        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+    for (int u = 0; u < NPW; ++u) {
+        pc.gA[u] = piece_off<BT, KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<BT, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
         pc.offA[u] = (int)(pc.gA[u] * 8);
         pc.offB[u] = (int)(pc.gB[u] * 8);
     }
-    f64x4 acc[4][4];
+    f64x4 acc[MI][MI];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < MI; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
+        for (int b = 0; b < MI; ++b) acc[a][b] = f64x4{0, 0, 0, 0};
 
     const int nt = (int)(p.k / RBK);
     auto kt = [&](int t) { return (i64)min(t, nt - 1) * RBK; };
@@ -395,18 +426,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) piece<BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+        for (int u = 0; u < NPW; ++u)
+            piece<BT, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            piece<BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+        for (int u = 0; u < NPW; ++u)
+            piece<BT, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
     }
-    wait_cnt<16, NOWAIT_LGKM>();
+    wait_cnt<2 * NPW, NOWAIT_LGKM>();
     dma_barrier();
-    Ops X, Y;
+    Ops<BT> X, Y;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        X.a[q] = ropnd<KCA>(lds, wr * WT + q * 16, 0, l);
-        X.b[q] = ropnd<KCB>(lds + UNIT, wc * WT + q * 16, 0, l);
+    for (int q = 0; q < MI; ++q) {
+        X.a[q] = ropnd<BT, KCA>(lds, wr * WT + q * 16, 0, l);
+        X.b[q] = ropnd<BT, KCB>(lds + UNIT, wc * WT + q * 16, 0, l);
     }
     wait_cnt<NOWAIT_VM, 0>();
     auto ktile = [&](auto jc, int t) {
@@ -416,26 +448,33 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
         lds_char* rA = lds + sA * UNIT;
         lds_char* rB = lds + sB * UNIT;
         const i64 k2 = kt(t + 2);
-        // (t,0..3): operands of (t,1..4); two pieces of A_{t+2} each
-        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 1, lds + st0 * UNIT, 0, k2, acc, X, Y);
-        wait_cnt<NOWAIT_VM, 0>();
-        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 2, lds + st0 * UNIT, 2, k2, acc, Y, X);
-        wait_cnt<NOWAIT_VM, 0>();
-        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 3, lds + st0 * UNIT, 4, k2, acc, X, Y);
-        wait_cnt<NOWAIT_VM, 0>();
-        ring::kstep<KCA, KCB, BUF, false, 2>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 4, lds + st0 * UNIT, 6, k2, acc, Y, X);
-        wait_cnt<NOWAIT_VM, 0>();
-        // (t,4..6): operands of (t,5..7), no staging
-        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 5, lds, 0, k2, acc, X, Y);
-        wait_cnt<NOWAIT_VM, 0>();
-        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 6, lds, 0, k2, acc, Y, X);
-        wait_cnt<NOWAIT_VM, 0>();
-        ring::kstep<KCA, KCB, BUF, false, 0>(p, m0, n0, w, l, wr, wc, pc, rA, rB, 7, lds, 0, k2, acc, X, Y);
-        wait_cnt<8, 0>();
+        // (t,0..NKS-2): operands of (t,1..NKS-1) from A_t, B_t; the pieces of A_{t+2}
+        // over the first NKS/2 k-steps (operands alternate X -> Y -> X; NKS is even)
+        auto ks = [&](auto sc) {
+            constexpr int S = decltype(sc)::value;
+            constexpr int NP = S < NKS / 2 ? NPA : 0;
+            if constexpr (S % 2 == 0)
+                ring::kstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
+                                                          lds + st0 * UNIT, S * NPA, k2, acc, X, Y);
+            else
+                ring::kstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
+                                                          lds + st0 * UNIT, S * NPA, k2, acc, Y, X);
+            if constexpr (S < NKS - 2) wait_cnt<NOWAIT_VM, 0>();
+        };
+        ks(std::integral_constant<int, 0>{});
+        ks(std::integral_constant<int, 1>{});
+        ks(std::integral_constant<int, 2>{});
+        if constexpr (NKS == 8) {
+            ks(std::integral_constant<int, 3>{});
+            ks(std::integral_constant<int, 4>{});
+            ks(std::integral_constant<int, 5>{});
+            ks(std::integral_constant<int, 6>{});
+        }
+        wait_cnt<NPW, 0>();  // A_{t+1}, B_{t+1} landed (A_{t+2} may fly); reads of A_t, B_t retired
         dma_barrier();
-        // (t,7): operands of (t+1,0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
-        ring::kstep<KCA, KCB, BUF, true, 8>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
-                                            lds + st1 * UNIT, 0, k2, acc, Y, X);
+        // (t,NKS-1): operands of (t+1,0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
+        ring::kstep<BT, KCA, KCB, BUF, true, NPW>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT,
+                                                  0, lds + st1 * UNIT, 0, k2, acc, Y, X);
         wait_cnt<NOWAIT_VM, 0>();
     };
     for (int t = 0; t < nt; t += NSLOT) {
@@ -450,18 +489,18 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
     // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
     const int g = l >> 4, c = l & 15;
     const i64 ib = m0 + wr * WT, jb = n0 + wc * WT;
-    if (m0 + 128 <= p.m && n0 + 128 <= p.n) {
+    if (m0 + BT <= p.m && n0 + BT <= p.n) {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-            double cv[4][4];
+        for (int mi = 0; mi < MI; ++mi) {
+            double cv[MI][4];
             if (!BETA0) {
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r];
             }
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const double v = p.alpha * acc[mi][ni][r];
@@ -471,9 +510,9 @@ __global__ __launch_bounds__(256, 1) void gemm_f64r_kernel(GParams p) {
         return;
     }
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
+        for (int ni = 0; ni < MI; ++ni) {
             const i64 j = jb + ni * 16 + c;
             if (j >= p.n) continue;
             double* col = p.C + j * p.ldc;
@@ -512,18 +551,19 @@ hipError_t launch_g(GParams p, hipStream_t s) {
     return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
 
-template <bool KCA, bool KCB>
+template <int BT, bool KCA, bool KCB>
 hipError_t launch_r(GParams p, hipStream_t s) {
-    p.tiles_m = (int)((p.m + 127) / 128);
-    p.tiles_n = (int)((p.n + 127) / 128);
+    constexpr int RBK = ring::RG<BT>::RBK;
+    p.tiles_m = (int)((p.m + BT - 1) / BT);
+    p.tiles_n = (int)((p.n + BT - 1) / BT);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    const bool buf = dma_fits(KCA ? 128 : ring::RBK, p.lda, 8) && dma_fits(KCB ? 128 : ring::RBK, p.ldb, 8);
+    const bool buf = dma_fits(KCA ? BT : RBK, p.lda, 8) && dma_fits(KCB ? BT : RBK, p.ldb, 8);
     if (p.beta == 0.0) {
-        if (buf) return launch(gemm_f64r_kernel<KCA, KCB, true, true>, grid, 256, p, s);
-        return launch(gemm_f64r_kernel<KCA, KCB, true, false>, grid, 256, p, s);
+        if (buf) return launch(gemm_f64r_kernel<BT, KCA, KCB, true, true>, grid, 256, p, s);
+        return launch(gemm_f64r_kernel<BT, KCA, KCB, true, false>, grid, 256, p, s);
     }
-    if (buf) return launch(gemm_f64r_kernel<KCA, KCB, false, true>, grid, 256, p, s);
-    return launch(gemm_f64r_kernel<KCA, KCB, false, false>, grid, 256, p, s);
+    if (buf) return launch(gemm_f64r_kernel<BT, KCA, KCB, false, true>, grid, 256, p, s);
+    return launch(gemm_f64r_kernel<BT, KCA, KCB, false, false>, grid, 256, p, s);
 }
 
 template <typename SH>
@@ -545,15 +585,20 @@ bool t64_tiles(i64 m, i64 n) {
     return prefer_t64(v, m, n, 255);
 }
 
-// the ring kernel (128 x 128 tiles, 32-deep K-tiles) on every 128-tile grid;
-// ELX_F64G_RING = 0 falls back to the two-stage slab kernel (read per call, for
-// the A/B and the tests).  Measured against the slab kernel in one process
-// (profiles/r05o_ring_ab.log): 32768^3 NN 73.7 -> 74.0 TF, 16384^3 NN / TN / NT /
-// TT 73.8 / 68.7 / 71.9 / 73.1 -> 74.6 / 76.1 / 72.6 / 74.3, 4096^3 70.4 -> 72.1.
-bool ring_tiles(i64 m, i64 n) {
+// the ring kernel's tile edge for this grid (0: the slab kernel).  128: the
+// ring on every grid of 128-tiles; measured against the slab kernel in one
+// process (profiles/r05o_ring_ab.log): 32768^3 NN 73.7 -> 74.0 TF, 16384^3 NN /
+// TN / NT / TT 73.8 / 68.7 / 71.9 / 73.1 -> 74.6 / 76.1 / 72.6 / 74.3, 4096^3
+// 70.4 -> 72.1 (and with the RC images in 256-B lines 76.5-76.7 in every
+// orientation, profiles/r05aa_f64_rcblk_ab.log).  64: the 64 x 64 ring on grids
+// of 64-tiles (four workgroups per CU), where it measured ahead of the slab
+// kernel (profiles/r05af_f64_ring64_ab.log).  ELX_F64G_RING (read per call, for
+// the A/B and the tests): bit 0 the 128 ring, bit 1 the 64 ring, 0 neither.
+int ring_bt(i64 m, i64 n) {
     const char* e = getenv("ELX_F64G_RING");
-    const int v = e ? atoi(e) : 1;
-    return v == 1 && !t64_tiles(m, n);
+    const int v = e ? atoi(e) : RING64_DEFAULT ? 3 : 1;
+    if (t64_tiles(m, n)) return (v & 2) ? 64 : 0;
+    return (v & 1) ? 128 : 0;
 }
 
 }  // namespace
@@ -563,8 +608,9 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
                     (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
-    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
-    if (ring_tiles(m, n)) return dma_plan(ok && k >= ring::RBK, (m + 127) / 128 * ((n + 127) / 128), k, ring::RBK, 256);
+    const int bt = ring_bt(m, n);
+    if (bt == 128) return dma_plan(ok && k >= 32, (m + 127) / 128 * ((n + 127) / 128), k, 32, 256);
+    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK, bt == 64 ? 1024 : 512);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 
@@ -585,9 +631,14 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // TT 65.0 vs 62.2); profiles/r04_t64_waves8_ab.log (the fp32 kernel measured
     // 4-13 % slower with eight and keeps four).  ELX_F64G_T64W = 4 / 8 forces one.
     static const int t64w = [] { const char* v = getenv("ELX_F64G_T64W"); return v ? atoi(v) : 0; }();
-    if (ring_tiles(m, n) && kmain % ring::RBK == 0 && kchunk % ring::RBK == 0) {
-        if (ta) return !tb ? launch_r<true, true>(p, s) : launch_r<true, false>(p, s);
-        return !tb ? launch_r<false, true>(p, s) : launch_r<false, false>(p, s);
+    const int bt = ring_bt(m, n);
+    if (bt == 128 && kmain % 32 == 0 && kchunk % 32 == 0) {
+        if (ta) return !tb ? launch_r<128, true, true>(p, s) : launch_r<128, true, false>(p, s);
+        return !tb ? launch_r<128, false, true>(p, s) : launch_r<128, false, false>(p, s);
+    }
+    if (bt == 64 && kmain % 16 == 0 && kchunk % 16 == 0) {
+        if (ta) return !tb ? launch_r<64, true, true>(p, s) : launch_r<64, true, false>(p, s);
+        return !tb ? launch_r<64, false, true>(p, s) : launch_r<64, false, false>(p, s);
     }
     if (t64_tiles(m, n)) {
         if (t64w == 8 || (t64w != 4 && !ta)) return launch_shape<Shape<64, 32, BK, 64, 16>>(ta, !tb, p, s);

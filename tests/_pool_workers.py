@@ -1,8 +1,9 @@
 """Subprocess bodies of the allocator hazard tests (tests/test_gpu_kernels.py).
 
-Each runs in a fresh process because the pool's knobs (ELX_POOL_RELEASE_THRESHOLD,
-ELX_POOL_CACHE, H_CUB_DEBUG) are read once, when the library first touches the
-GPU.  `python tests/_pool_workers.py <case>` prints "OK <case>" on success.
+Each runs in a fresh process because the pool's knobs (ELX_POOL_CACHE, H_CUB_DEBUG)
+are read once, when the library first touches the GPU.  ELX_POOL_CACHE=0 is the
+regime round 4's release threshold 0 stood for: every freed block goes back to
+the driver (hipFree) at once, so a premature reuse is as likely as it gets.  `python tests/_pool_workers.py <case>` prints "OK <case>" on success.
 
 The hazard (round 4's wrong GEMMs): a block whose last reader runs on a stream
 that is not ordered before the stream it is freed on.  A spin kernel delays the

@@ -157,9 +157,11 @@ def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
 
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-@pytest.mark.parametrize("shape,beta", [((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0), ((2048, 4096, 2072), -1.0),
-                                        ((4096, 2048, 32), 0.5)])
-@pytest.mark.parametrize("ring", ["1", "0"])
+@pytest.mark.parametrize("ring,shape,beta", [
+    (r, sh, b) for r in ("1", "0") for sh, b in [((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0),
+                                                 ((2048, 4096, 2072), -1.0), ((4096, 2048, 32), 0.5)]] + [
+    ("2", (1536, 2048, 640), -1.0), ("2", (1000, 1016, 1056), 0.0), ("2", (1536, 2048, 2072), -1.0),
+    ("2", (1024, 512, 16), 0.5)])
 def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     """The fp64 ring kernel (gemm_f64r_kernel: four waves, a 5-slot LDS ring of
     32-deep K-tiles; ELX_F64G_RING=1) on 128-tile grids: many wraps of the ring
@@ -167,7 +169,10 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     not be read), the k % 32 tail through the general kernel (2072 = 64 x 32 +
     24), and a single K-tile (k = 32: prologue and clamped restaging only).
     Integer operands: exact in every orientation.  ring = "0": the same cases
-    through the two-stage slab kernel it replaced as the default."""
+    through the two-stage slab kernel it replaced as the default; ring = "2":
+    the 64 x 64 ring (16-deep K-tiles, four workgroups per CU) on grids of
+    64-tiles, likewise with a ragged grid, a k tail (2072 = 129 x 16 + 8) and a
+    single K-tile."""
     monkeypatch.setenv("ELX_F64G_RING", ring)
     m, n, k = shape
     rng = np.random.default_rng(m + k)
