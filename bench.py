@@ -43,10 +43,8 @@ sys.path.insert(0, ROOT)
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3, "bf16": 2500.0, "f16": 2500.0}
 HBM_PEAK_GBS = 8000.0
 METRIC = "distributed Gemm TFLOP/s (fp64/fp32) at 1/2/4/8 GPUs; % of MFMA peak"
-KERNEL = {"f64": "gemm_f64r_kernel (LDS-DMA ring)", "f32": "gemm_f32g_kernel (LDS-DMA slab)",
+KERNEL = {"f64": "gemm_f64r_kernel (LDS-DMA ring)", "f32": "gemm_f32r_kernel (LDS-DMA ring)",
           "bf16": "gemm_h4w_kernel<bf16> (four-wave)", "f16": "gemm_h4w_kernel<f16> (four-wave)"}
-# fp32 with both local operands k-contiguous (C4's TN) runs the ring kernel
-KERNEL_F32_TN = "gemm_f32r_kernel (LDS-DMA ring)"
 
 
 _WATCHDOG = None  # elemental_amd.el once imported
@@ -314,7 +312,7 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
     out = {"workload": workload, "value": round(value, 3), "unit": "TFLOP/s", "dtype": dtype, "steps": steps,
            "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
            "pct_of_mfma_peak": round(100.0 * value / (PEAK_TFLOPS[dtype] * world), 2),
-           "roofline": {"bound": "mfma", "kernel": KERNEL_F32_TN if config == "c4" else KERNEL[dtype],
+           "roofline": {"bound": "mfma", "kernel": KERNEL[dtype],
                         "achieved": round(ach, 3), "peak": PEAK_TFLOPS[dtype], "frac": round(ach / PEAK_TFLOPS[dtype], 4),
                         "launches_timed": prof["launches"], "avg_launch_ms": round(avg_ms, 3)}}
     if world > 1:
@@ -500,7 +498,7 @@ def main():
         "pct_of_mfma_peak": round(100.0 * value / (peak * world), 2),
         "roofline": {
             "bound": "mfma",
-            "kernel": f"{KERNEL_F32_TN if config == 'c4' and dtype == 'f32' else KERNEL[dtype]} (local panel update)",
+            "kernel": f"{KERNEL[dtype]} (local panel update)",
             "achieved": round(achieved, 3),
             "peak": peak,
             "unit": "TFLOP/s",

@@ -286,13 +286,19 @@ __global__ __launch_bounds__(SH::NT, SH::MINB) void gemm_f32g_kernel(FParams p) 
 // The hazard argument is gemm_f64r_kernel's (gemm_f64g.hip).
 // ---------------------------------------------------------------------------
 namespace fring {
-constexpr int NSLOT = 5, UNIT = 32 * 1024;
-template <int BT>
+constexpr int NSLOT = 5;
+// UN: bytes of one operand image (32 KiB: one workgroup per CU; 8 KiB: the 64 x 64
+// tiles with 32-deep K-tiles, four workgroups per CU)
+template <int BT, int UN>
 struct G {
-    static constexpr int RBK = UNIT / 4 / BT, WT = BT / 2, MI = WT / 16, NQ = RBK / 16, KS = RBK / 4;
+    static constexpr int UNIT = UN, NPW = UN / 1024 / 4, MINB = 32768 / UN;
+    static constexpr int RBK = UN / 4 / BT, WT = BT / 2, MI = WT / 16, NQ = RBK / 16, KS = RBK / 4;
     static constexpr int NM = 4 * MI * MI, NR = 2 * MI;  // MFMAs and fragment reads per quad
 };
-__device__ __forceinline__ int swz_r(int r) { return r & 15; }
+// KC rows of CPR 16-B chunks: c ^ (r & 15), or (r >> 1) & 7 for 128-B rows (the 16
+// lanes of a b128 read then hit 16 distinct chunk slots either way)
+template <int CPR>
+__device__ __forceinline__ int swz_r(int r) { return CPR >= 16 ? r & 15 : (r >> 1) & 7; }
 template <int RBK>
 __device__ __forceinline__ int swz_k(int kk) { return ((kk / (RBK / 4)) & 3) << 2; }
 
@@ -301,14 +307,14 @@ __device__ __forceinline__ int swz_k(int kk) { return ((kk / (RBK / 4)) & 3) << 
 // piece (BT 128) measured 3.5-6 % slower, as in the fp64 ring
 // (profiles/r05ab_f32_lines_ab.log, r05aa_f64_rcblk_ab.log).
 // per-lane element offset of piece `ins` (0..31) of one operand's K-tile image
-template <int BT, bool KC>
+template <int BT, int UN, bool KC>
 __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
-    constexpr int RBK = G<BT>::RBK, KS = G<BT>::KS;
+    constexpr int RBK = G<BT, UN>::RBK, KS = G<BT, UN>::KS;
     if (KC) {  // whole rows of RBK floats, RPI rows per piece (the 256-B lines of
                // 512-B rows measured slower at BT 64: TN 1024^2 x 2048 124 -> 120 TF)
         constexpr int CPR = RBK / 4, RPI = 64 / CPR;
         const int r = ins * RPI + l / CPR;
-        const int c = (l % CPR) ^ swz_r(r);
+        const int c = (l % CPR) ^ swz_r<CPR>(r);
         const i64 row = R0 + r < rows ? r : rows - 1 - R0;
         return row * ld + 4 * c;
     } else {   // k-rows 4 kq.. of BT floats, line ins % NSEG; chunk ^ 4 g(kq)
@@ -321,12 +327,12 @@ __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 l
     }
 }
 
-template <int BT, bool BUF, bool KC>
+template <int BT, int UN, bool BUF, bool KC>
 __device__ __forceinline__ void piece(const float* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int ins,
                                       lds_char* img) {
     const float* base = KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
     if constexpr (BUF) {
-        const BufferSrc<float> src(base, (KC ? BT : G<BT>::RBK) * ld * 4);
+        const BufferSrc<float> src(base, (KC ? BT : G<BT, UN>::RBK) * ld * 4);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + ins * 1024),
                                                  16, off, 0, 0, 0);
     } else {
@@ -336,13 +342,14 @@ __device__ __forceinline__ void piece(const float* X, i64 ld, i64 R0, i64 k0, in
 }
 
 // quad j's four values of one 16-row fragment: v[e] = X(R0 + (l&15), KS (l>>4) + 4 j + e)
-template <int BT, bool KC>
+template <int BT, int UN, bool KC>
 __device__ __forceinline__ void quad(const lds_char* img, int R0, int j, int l, float (&v)[4]) {
-    constexpr int RBK = G<BT>::RBK, KS = G<BT>::KS;
+    constexpr int RBK = G<BT, UN>::RBK, KS = G<BT, UN>::KS;
     const int r = R0 + (l & 15), g = l >> 4;
     if (KC) {
+        constexpr int CPR = RBK / 4;
         const int c = (KS / 4) * g + j;
-        const f32x4 x = *(const __attribute__((address_space(3))) f32x4*)(img + r * (RBK * 4) + ((c ^ swz_r(r)) << 4));
+        const f32x4 x = *(const __attribute__((address_space(3))) f32x4*)(img + r * (RBK * 4) + ((c ^ swz_r<CPR>(r)) << 4));
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = x[e];
     } else {
@@ -357,21 +364,22 @@ __device__ __forceinline__ void quad(const lds_char* img, int R0, int j, int l, 
     }
 }
 
-template <int BT>
-struct Ops { float a[G<BT>::MI][4], b[G<BT>::MI][4]; };
-struct Pieces { int offA[8], offB[8]; i64 gA[8], gB[8]; };
+template <int BT, int UN>
+struct Ops { float a[G<BT, UN>::MI][4], b[G<BT, UN>::MI][4]; };
+template <int NPW>
+struct Pieces { int offA[NPW], offB[NPW]; i64 gA[NPW], gB[NPW]; };
 
 // one quad: the MFMAs of four k-steps on `cur`; quad `jrd` of rdA / rdB into
 // `nxt` over the first half of them (fragment f after MFMA f MI); NP pieces u0..
 // of one unit into `st` over the second half (SB: of B, else of A).  Unrolled
 // by a fold over the MFMA index, not a loop: the placement is then constexpr.
-template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
+template <int BT, int UN, bool KCA, bool KCB, bool BUF, bool SB, int NP>
 struct Quad {
-    static constexpr int MI = G<BT>::MI, NM = G<BT>::NM, NR = G<BT>::NR, WT = G<BT>::WT, H = NM / 2;
+    static constexpr int MI = G<BT, UN>::MI, NM = G<BT, UN>::NM, NR = G<BT, UN>::NR, WT = G<BT, UN>::WT, H = NM / 2;
     const FParams& p;
     i64 m0, n0;
     int w, l, wr, wc;
-    const Pieces& pc;
+    const Pieces<G<BT, UN>::NPW>& pc;
     const lds_char* __restrict__ rdA;
     const lds_char* __restrict__ rdB;
     int jrd;
@@ -380,42 +388,44 @@ struct Quad {
     i64 k0;
 
     template <int I>
-    __device__ __forceinline__ void step(f32x4 (&acc)[MI][MI], const Ops<BT>& cur, Ops<BT>& nxt) const {
+    __device__ __forceinline__ void step(f32x4 (&acc)[MI][MI], const Ops<BT, UN>& cur, Ops<BT, UN>& nxt) const {
         constexpr int e = I / (MI * MI), mi = (I / MI) % MI, ni = I % MI;
         acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.a[mi][e], cur.b[ni][e], acc[mi][ni], 0, 0, 0);
         if constexpr (I % MI == 0 && I / MI < NR) {
             constexpr int f = I / MI;
-            if constexpr (f < MI) quad<BT, KCA>(rdA, wr * WT + f * 16, jrd, l, nxt.a[f]);
-            else quad<BT, KCB>(rdB, wc * WT + (f - MI) * 16, jrd, l, nxt.b[f - MI]);
+            if constexpr (f < MI) quad<BT, UN, KCA>(rdA, wr * WT + f * 16, jrd, l, nxt.a[f]);
+            else quad<BT, UN, KCB>(rdB, wc * WT + (f - MI) * 16, jrd, l, nxt.b[f - MI]);
         }
         if constexpr (NP > 0 && I >= H && (I - H) % (H / NP) == 0) {
             const int u = u0 + (I - H) / (H / NP);
-            if constexpr (SB) piece<BT, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-            else piece<BT, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+            if constexpr (SB) piece<BT, UN, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+            else piece<BT, UN, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the placement as written
     }
     template <int... Is>
-    __device__ __forceinline__ void run(f32x4 (&acc)[MI][MI], const Ops<BT>& cur, Ops<BT>& nxt,
+    __device__ __forceinline__ void run(f32x4 (&acc)[MI][MI], const Ops<BT, UN>& cur, Ops<BT, UN>& nxt,
                                         std::integer_sequence<int, Is...>) const {
         (step<Is>(acc, cur, nxt), ...);
     }
 };
 
-template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
+template <int BT, int UN, bool KCA, bool KCB, bool BUF, bool SB, int NP>
 __device__ __forceinline__ void qstep(const FParams& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
-                                      const Pieces& pc, const lds_char* __restrict__ rdA,
+                                      const Pieces<G<BT, UN>::NPW>& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int jrd, lds_char* __restrict__ st, int u0,
-                                      i64 k0, f32x4 (&acc)[G<BT>::MI][G<BT>::MI], const Ops<BT>& cur, Ops<BT>& nxt) {
-    const Quad<BT, KCA, KCB, BUF, SB, NP> q{p, m0, n0, w, l, wr, wc, pc, rdA, rdB, jrd, st, u0, k0};
-    q.run(acc, cur, nxt, std::make_integer_sequence<int, G<BT>::NM>{});
+                                      i64 k0, f32x4 (&acc)[G<BT, UN>::MI][G<BT, UN>::MI], const Ops<BT, UN>& cur, Ops<BT, UN>& nxt) {
+    const Quad<BT, UN, KCA, KCB, BUF, SB, NP> q{p, m0, n0, w, l, wr, wc, pc, rdA, rdB, jrd, st, u0, k0};
+    q.run(acc, cur, nxt, std::make_integer_sequence<int, G<BT, UN>::NM>{});
 }
 }  // namespace fring
 
-template <int BT, bool KCA, bool KCB, bool BETA0, bool BUF>
-__global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
+template <int BT, int UN, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(256, (fring::G<BT, UN>::MINB)) void gemm_f32r_kernel(FParams p) {
     using namespace fring;
-    constexpr int RBK = G<BT>::RBK, WT = G<BT>::WT, MI = G<BT>::MI, NQ = G<BT>::NQ, PPQ = 16 / NQ;
+    using Gm = G<BT, UN>;
+    constexpr int RBK = Gm::RBK, WT = Gm::WT, MI = Gm::MI, NQ = Gm::NQ, UNIT = Gm::UNIT, NPW = Gm::NPW;
+    constexpr int PPQ = NPW / (NQ / 2);  // pieces of A_{t+2} per quad over the first half
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
     lds_char* lds = (lds_char*)lds_raw;
     const int tid = threadIdx.x, l = tid & 63;
@@ -431,11 +441,11 @@ __global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
         p.B += KCB ? kz0 : kz0 * p.ldb;
         p.C += (i64)blockIdx.y * p.zstride;
     }
-    Pieces pc;
+    Pieces<NPW> pc;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        pc.gA[u] = piece_off<BT, KCA>(w + 4 * u, l, m0, p.m, p.lda);
-        pc.gB[u] = piece_off<BT, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+    for (int u = 0; u < NPW; ++u) {
+        pc.gA[u] = piece_off<BT, UN, KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<BT, UN, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
         pc.offA[u] = (int)(pc.gA[u] * 4);
         pc.offB[u] = (int)(pc.gB[u] * 4);
     }
@@ -451,19 +461,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            piece<BT, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+        for (int u = 0; u < NPW; ++u)
+            piece<BT, UN, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            piece<BT, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+        for (int u = 0; u < NPW; ++u)
+            piece<BT, UN, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
     }
-    wait_cnt<16, NOWAIT_LGKM>();
+    wait_cnt<2 * NPW, NOWAIT_LGKM>();
     dma_barrier();
-    Ops<BT> X, Y;
+    Ops<BT, UN> X, Y;
 #pragma unroll
     for (int f = 0; f < MI; ++f) {
-        quad<BT, KCA>(lds, wr * WT + f * 16, 0, l, X.a[f]);
-        quad<BT, KCB>(lds + UNIT, wc * WT + f * 16, 0, l, X.b[f]);
+        quad<BT, UN, KCA>(lds, wr * WT + f * 16, 0, l, X.a[f]);
+        quad<BT, UN, KCB>(lds + UNIT, wc * WT + f * 16, 0, l, X.b[f]);
     }
     wait_cnt<NOWAIT_VM, 0>();
     auto ktile = [&](auto jc, int t) {
@@ -478,26 +488,28 @@ __global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
             constexpr int Q = decltype(qc)::value;
             constexpr int NP = Q < NQ / 2 ? PPQ : 0;
             if constexpr (Q % 2 == 0)
-                qstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
+                qstep<BT, UN, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
                                                     Q * PPQ, k2, acc, X, Y);
             else
-                qstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
+                qstep<BT, UN, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, Q + 1, lds + st0 * UNIT,
                                                     Q * PPQ, k2, acc, Y, X);
             if constexpr (Q < NQ - 2) wait_cnt<NOWAIT_VM, 0>();
         };
         q(std::integral_constant<int, 0>{});
-        q(std::integral_constant<int, 1>{});
-        q(std::integral_constant<int, 2>{});
+        if constexpr (NQ >= 4) {
+            q(std::integral_constant<int, 1>{});
+            q(std::integral_constant<int, 2>{});
+        }
         if constexpr (NQ == 8) {
             q(std::integral_constant<int, 3>{});
             q(std::integral_constant<int, 4>{});
             q(std::integral_constant<int, 5>{});
             q(std::integral_constant<int, 6>{});
         }
-        wait_cnt<8, 0>();
+        wait_cnt<NPW, 0>();
         dma_barrier();
         // quad NQ-1: quad (t+1, 0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
-        qstep<BT, KCA, KCB, BUF, true, 8>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+        qstep<BT, UN, KCA, KCB, BUF, true, NPW>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
                                           lds + st1 * UNIT, 0, k2, acc, Y, X);
         wait_cnt<NOWAIT_VM, 0>();
     };
@@ -549,19 +561,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f32r_kernel(FParams p) {
         }
 }
 
-template <int BT, bool KCA, bool KCB>
+template <int BT, int UN, bool KCA, bool KCB>
 hipError_t launch_fr(FParams p, hipStream_t s) {
-    constexpr int RBK = fring::G<BT>::RBK;
+    constexpr int RBK = fring::G<BT, UN>::RBK;
     p.tiles_m = (int)((p.m + BT - 1) / BT);
     p.tiles_n = (int)((p.n + BT - 1) / BT);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
     const bool buf = dma_fits(KCA ? BT : RBK, p.lda, 4) && dma_fits(KCB ? BT : RBK, p.ldb, 4);
     if (p.beta == 0.f) {
-        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
+        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, UN, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, UN, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
     } else {
-        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
+        if (buf) hipLaunchKernelGGL((gemm_f32r_kernel<BT, UN, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((gemm_f32r_kernel<BT, UN, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
     }
     return hipGetLastError();
 }
@@ -579,9 +591,14 @@ hipError_t launch_fw(FParams p, hipStream_t s) {
 
 // 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU, whole k) where
 // prefer_t64 (kernels.hpp) says they balance the CUs better; ELX_F32G_T64 = 0
-// never, 2 always (tests).
-bool t64_tiles(i64 m, i64 n) {
+// never, 2 always (tests).  A grid of exactly 256 128-tiles (2048^2) takes them
+// too when k is short (2048^3 NN 135.6 -> 140.9 TF, TN 141.3 -> 141.8; at
+// 2048^2 x 16384 the 128-tiles stay ahead, 144.0 vs 141.2;
+// profiles/r05ai_f32_t64_rule_ab.log).  k compared as k / 64 * 64, so that the
+// plan (k) and the launch (its kmain) decide alike.
+bool t64_tiles(i64 m, i64 n, i64 k) {
     static const int v = [] { const char* e = getenv("ELX_F32G_T64"); return e ? atoi(e) : 1; }();
+    if (v == 1 && (m + 127) / 128 * ((n + 127) / 128) == 256 && k / 64 * 64 <= 4096) return true;
     return prefer_t64(v, m, n);
 }
 
@@ -596,17 +613,33 @@ bool t64_tiles(i64 m, i64 n) {
 //    145.3 -> 146.2; with A rows-contiguous (NN, NT) the slab kernel's two
 //    workgroups per CU stay ahead below 16384^3 (C3-f32's 65536 x 8192^2 panel
 //    150.1 vs 147.6, 8192^3 149.8 vs 147.4, 4096^3 NN 146.9 vs 145.4).
+//  * 64 x 64 ring with 32-deep K-tiles (8 KiB images), four workgroups per CU
+//    ("65" below), on every grid of 64-tiles since it beats both (one process,
+//    profiles/r05ah_f32_ring65_ab.log): 1536 x 2048^2 NN / TN / NT / TT 127 / 129 /
+//    128 / 126 (slab) -> 143 / 143 / 142 / 142 TF, 3072^3 135 -> 148, 2560^3 118 ->
+//    133, 1536^3 93 -> 106, 1024^3 109 -> 116, 1024^2 x 2048 123.3 (one per CU)
+//    -> 124.0.
+//  * 128 x 128 ring with 32-deep K-tiles (16 KiB images), two workgroups per CU
+//    ("129"), on grids of >= 512 128-tiles, every orientation
+//    (profiles/r05aj_f32_ring129_ab.log): 16384^3 NN / NT / TN / TT (slab or
+//    one-per-CU ring) 150.7 / 149.5 / 151.3 / 149.7 -> 153.9 / 154.0 / 153.6 /
+//    153.7 TF, 4096^3 NN 146.6 -> 150.6, C3-f32's 65536 x 8192^2 panel 150.1 ->
+//    153.2, C4's TN 8192^2 x 65536 151.8 -> 151.4; with fewer tiles the one-per-
+//    CU ring keeps whole k (2048^2 x 16384 NN 147.2 vs 146.5 split, 143.4 slab).
 // ELX_F32G_RING (read per call, for the A/B and the tests) overrides: bit 0 the
-// 128 x 128 ring on every grid of 128-tiles, bit 1 the 64 x 64 ring on every
-// grid of 64-tiles, 0 neither.
-int ring_bt(bool kca, bool kcb, i64 m, i64 n) {
+// one-per-CU 128 x 128 ring and bit 3 the two-per-CU one on every grid of
+// 128-tiles, bit 1 the one-per-CU 64 x 64 ring and bit 2 the four-per-CU one on
+// grids of 64-tiles (both set: the first on grids of <= 256 64-tiles), 0 none.
+int ring_bt(bool kca, bool kcb, i64 m, i64 n, i64 k) {
     const char* e = getenv("ELX_F32G_RING");
-    if (t64_tiles(m, n)) {
-        if (e) return (atoi(e) & 2) ? 64 : 0;
-        return (m + 63) / 64 * ((n + 63) / 64) <= 256 ? 64 : 0;
+    if (t64_tiles(m, n, k)) {
+        const int v = e ? atoi(e) : 4;
+        const bool one_round = (m + 63) / 64 * ((n + 63) / 64) <= 256;
+        if ((v & 2) && ((v & 4) == 0 || one_round) && (e || one_round)) return 64;
+        return (v & 4) ? 65 : 0;
     }
-    if (e) return (atoi(e) & 1) ? 128 : 0;
-    return kca ? 128 : 0;
+    if (e) return (atoi(e) & 8) ? 129 : (atoi(e) & 1) ? 128 : 0;
+    return (m + 127) / 128 * ((n + 127) / 128) >= 512 ? 129 : 128;
 }
 
 template <bool KCA, bool KCB, bool BUF>
@@ -619,10 +652,12 @@ hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // profiles/r03_f32_wtm.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
-    const int bt = ring_bt(KCA, KCB, p.m, p.n);
-    if (bt == 128 && p.k % 64 == 0 && p.kchunk % 64 == 0) return launch_fr<128, KCA, KCB>(p, s);
-    if (bt == 64 && p.k % 128 == 0 && p.kchunk % 128 == 0) return launch_fr<64, KCA, KCB>(p, s);
-    if (t64_tiles(p.m, p.n)) {
+    const int bt = ring_bt(KCA, KCB, p.m, p.n, p.k);
+    if (bt == 128 && p.k % 64 == 0 && p.kchunk % 64 == 0) return launch_fr<128, 32768, KCA, KCB>(p, s);
+    if (bt == 64 && p.k % 128 == 0 && p.kchunk % 128 == 0) return launch_fr<64, 32768, KCA, KCB>(p, s);
+    if (bt == 65 && p.k % 32 == 0 && p.kchunk % 32 == 0) return launch_fr<64, 8192, KCA, KCB>(p, s);
+    if (bt == 129 && p.k % 32 == 0 && p.kchunk % 32 == 0) return launch_fr<128, 16384, KCA, KCB>(p, s);
+    if (t64_tiles(p.m, p.n, p.k)) {
         // at most one workgroup per CU: a 4-slab LDS ring unless NN (NT 1024^2 x
         // 2048 72.7 -> 93.7 TF, TN 96.4 -> 99.8, NN even; the fp64 kernel lost
         // with it; profiles/r04_small_ring_ab.log)
@@ -651,12 +686,14 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 4 == 0 && ldb % 4 == 0 && (kca || (m % 4 == 0 && m >= 4)) &&
                     (kcb || (n % 4 == 0 && n >= 4)) && m < (1ll << 31) && n < (1ll << 31);
-    const int bt = ring_bt(kca, kcb, m, n);
+    const int bt = ring_bt(kca, kcb, m, n, k);
+    if (bt == 65) return dma_plan(ok && k >= 32, (m + 63) / 64 * ((n + 63) / 64), k, 32, 1024);
+    if (bt == 129) return dma_plan(ok && k >= 32, (m + 127) / 128 * ((n + 127) / 128), k, 32, 512);
     if (bt) {  // one workgroup per CU, K-tiles of 8192 / bt
         const int rbk = 8192 / bt;
         return dma_plan(ok && k >= rbk, (m + bt - 1) / bt * ((n + bt - 1) / bt), k, rbk, 256);
     }
-    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
+    if (t64_tiles(m, n, k)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 

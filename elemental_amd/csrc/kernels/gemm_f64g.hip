@@ -574,14 +574,16 @@ hipError_t launch_shape(bool kca, bool kcb, const GParams& p, hipStream_t s) {
 
 bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-// 64 x 64 tiles (four waves of 32 x 32, four workgroups per CU, whole k) where
-// prefer_t64 (kernels.hpp) says they balance the CUs better; ELX_F64G_T64 = 0
-// never, 2 always (tests).
-// small = 255: a grid of exactly 256 128-tiles (2048^2) takes the ring kernel,
-// which beats the eight-wave 64 x 64 tiles there (NN 64.1 -> 69.3 TF, TN 63.3 ->
-// 70.9; profiles/r05o_ring_ab.log).
-bool t64_tiles(i64 m, i64 n) {
+// 64 x 64 tiles where prefer_t64 (kernels.hpp) says they balance the CUs
+// better; ELX_F64G_T64 = 0 never, 2 always (tests).  A grid of exactly 256
+// 128-tiles (2048^2) takes the 128 ring when k is long (2048^2 x 16384: 75.9 vs
+// 72.0 TF with the 64 ring) and the 64 ring, four workgroups per CU, when it is
+// short (2048^3 NN 70.7 -> 71.6, TN 70.7 -> 71.8; profiles/r05ag_f64_t64_rule_ab.log).
+// k: the depth the launch covers, compared as k / 32 * 32 so that the plan (k)
+// and the launch (its kmain) decide alike.
+bool t64_tiles(i64 m, i64 n, i64 k) {
     static const int v = [] { const char* e = getenv("ELX_F64G_T64"); return e ? atoi(e) : 1; }();
+    if (v == 1 && (m + 127) / 128 * ((n + 127) / 128) == 256 && k / 32 * 32 <= 4096) return true;
     return prefer_t64(v, m, n, 255);
 }
 
@@ -594,10 +596,10 @@ bool t64_tiles(i64 m, i64 n) {
 // of 64-tiles (four workgroups per CU), where it measured ahead of the slab
 // kernel (profiles/r05af_f64_ring64_ab.log).  ELX_F64G_RING (read per call, for
 // the A/B and the tests): bit 0 the 128 ring, bit 1 the 64 ring, 0 neither.
-int ring_bt(i64 m, i64 n) {
+int ring_bt(i64 m, i64 n, i64 k) {
     const char* e = getenv("ELX_F64G_RING");
     const int v = e ? atoi(e) : RING64_DEFAULT ? 3 : 1;
-    if (t64_tiles(m, n)) return (v & 2) ? 64 : 0;
+    if (t64_tiles(m, n, k)) return (v & 2) ? 64 : 0;
     return (v & 1) ? 128 : 0;
 }
 
@@ -608,9 +610,9 @@ DmaPlan gemm_f64_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const doubl
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 2 == 0 && ldb % 2 == 0 && (kca || (m % 2 == 0 && m >= 2)) &&
                     (kcb || (n % 2 == 0 && n >= 2)) && m < (1ll << 31) && n < (1ll << 31);
-    const int bt = ring_bt(m, n);
+    const int bt = ring_bt(m, n, k);
     if (bt == 128) return dma_plan(ok && k >= 32, (m + 127) / 128 * ((n + 127) / 128), k, 32, 256);
-    if (t64_tiles(m, n)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK, bt == 64 ? 1024 : 512);
+    if (t64_tiles(m, n, k)) return dma_plan(ok, (m + 63) / 64 * ((n + 63) / 64), k, BK, bt == 64 ? 1024 : 512);
     return dma_plan(ok, (m + 127) / 128 * ((n + 127) / 128), k, BK);
 }
 
@@ -631,7 +633,7 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     // TT 65.0 vs 62.2); profiles/r04_t64_waves8_ab.log (the fp32 kernel measured
     // 4-13 % slower with eight and keeps four).  ELX_F64G_T64W = 4 / 8 forces one.
     static const int t64w = [] { const char* v = getenv("ELX_F64G_T64W"); return v ? atoi(v) : 0; }();
-    const int bt = ring_bt(m, n);
+    const int bt = ring_bt(m, n, kmain);
     if (bt == 128 && kmain % 32 == 0 && kchunk % 32 == 0) {
         if (ta) return !tb ? launch_r<128, true, true>(p, s) : launch_r<128, true, false>(p, s);
         return !tb ? launch_r<128, false, true>(p, s) : launch_r<128, false, false>(p, s);
@@ -640,7 +642,7 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
         if (ta) return !tb ? launch_r<64, true, true>(p, s) : launch_r<64, true, false>(p, s);
         return !tb ? launch_r<64, false, true>(p, s) : launch_r<64, false, false>(p, s);
     }
-    if (t64_tiles(m, n)) {
+    if (t64_tiles(m, n, kmain)) {
         if (t64w == 8 || (t64w != 4 && !ta)) return launch_shape<Shape<64, 32, BK, 64, 16>>(ta, !tb, p, s);
         return launch_shape<Shape<64, 32, BK, 64, 32>>(ta, !tb, p, s);
     }

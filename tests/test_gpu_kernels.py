@@ -201,6 +201,8 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     ("1", (4096, 2048, 64), 0.5),
     ("2", (1024, 1024, 2048), -1.0), ("2", (1000, 1016, 1152), 0.0), ("2", (1536, 2048, 2100), -1.0),
     ("2", (1024, 512, 128), 0.5),
+    ("4", (1536, 2048, 640), -1.0), ("4", (1000, 1016, 1056), 0.0), ("4", (1536, 2048, 2100), -1.0),
+    ("4", (1024, 512, 32), 0.5),
     ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)])
 def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
     """The fp32 ring kernel (gemm_f32r_kernel; ELX_F32G_RING bit 0: 128 x 128
@@ -209,8 +211,9 @@ def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
     edge tiles with beta = 0 (C holds NaN and must not be read), the k tail
     through the general kernel (2072 = 32 x 64 + 24, 2100 = 16 x 128 + 52), a
     single K-tile (prologue and clamped restaging only), and the k-permuted
-    MFMA steps in every orientation.  ring = "0": the slab kernels on the ragged
-    cases.  Integer operands: exact."""
+    MFMA steps in every orientation.  ring = "4": the 64 x 64 ring with 32-deep
+    K-tiles and four workgroups per CU, likewise (2100 = 65 x 32 + 20).  ring =
+    "0": the slab kernels on the ragged cases.  Integer operands: exact."""
     monkeypatch.setenv("ELX_F32G_RING", ring)
     m, n, k = shape
     rng = np.random.default_rng(m + k + 1)
