@@ -277,19 +277,23 @@ constexpr int NSLOT = 5;
 // 32 x 32 (2 x 2 accumulators), K-tiles of 16 k (8 KiB per image, 40 KiB of
 // ring), four workgroups per CU, 4 k-steps of 4 MFMAs per K-tile; the same
 // schedule with 2 pieces per wave and image.
-template <int BT>
+// UN: bytes of one operand image (32 KiB: one workgroup per CU; 8 KiB: the 64 x 64
+// ring, four per CU).  (A 128 x 128 ring with 16 KiB images, two per CU, the
+// fp32 kernel's choice, measured 32768^3 76.3 -> 70.9 TF, 16384^3 -0.3..-1.8 %,
+// +0.5..1.3 % at 4096^2: not kept, profiles/r05ak_f64_ring129_ab.log.)
+template <int BT, int UN>
 struct RG {
-    static constexpr int RBK = BT == 128 ? 32 : 16, UNIT = BT * RBK * 8, WT = BT / 2, MI = WT / 16;
+    static constexpr int UNIT = UN, RBK = UN / 8 / BT, WT = BT / 2, MI = WT / 16;
     static constexpr int NKS = RBK / 4;                // k-steps per K-tile
     static constexpr int NPW = UNIT / 1024 / 4;        // pieces per wave and image
     static constexpr int NM = MI * MI, NR = 2 * MI;    // MFMAs and operand reads per k-step
-    static constexpr int MINB = BT == 128 ? 1 : 4;     // workgroups per CU
+    static constexpr int MINB = 32768 / UN;            // workgroups per CU
 };
 
 // per-lane element offset of piece `ins` of one operand's K-tile image
-template <int BT, bool KC>
+template <int BT, int UN, bool KC>
 __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 ld) {
-    constexpr int RBK = RG<BT>::RBK;
+    constexpr int RBK = RG<BT, UN>::RBK;
     if (KC) {  // RPI rows of RBK doubles per piece; chunk c of row r at c ^ swz_kc(r)
         constexpr int CPR = RBK / 2, RPI = 64 / CPR;
         const int r = ins * RPI + l / CPR;
@@ -310,21 +314,21 @@ __device__ __forceinline__ i64 piece_off(int ins, int l, i64 R0, i64 rows, i64 l
 }
 // operand of k-step s for rows R0..R0+15 from a ring image (KC: opnd's layout;
 // RC: the blocked layout above, 1-KiB block (s, r>>5), sub-row k & 3)
-template <int BT, bool KC>
+template <int BT, int UN, bool KC>
 __device__ __forceinline__ double ropnd(const lds_char* img, int R0, int s, int l) {
-    if (KC) return opnd<true, BT, RG<BT>::RBK>(img, R0, s, l);
+    if (KC) return opnd<true, BT, RG<BT, UN>::RBK>(img, R0, s, l);
     constexpr int NSEG = BT * 8 / 256;
     const int r = R0 + (l & 15), g = l >> 4;
     const int off = (s * NSEG + (r >> 5)) * 1024 + g * 256 + ((((r & 31) >> 1) ^ ((g & 1) << 3)) << 4) + ((r & 1) << 3);
     return *(const __attribute__((address_space(3))) double*)(img + off);
 }
 
-template <int BT, bool BUF, bool KC>
+template <int BT, int UN, bool BUF, bool KC>
 __device__ __forceinline__ void piece(const double* X, i64 ld, i64 R0, i64 k0, int off, i64 goff, int ins,
                                       lds_char* img) {
     const double* base = KC ? X + R0 * ld + k0 : X + R0 + k0 * ld;
     if constexpr (BUF) {
-        const BufferSrc<double> src(base, (KC ? BT : RG<BT>::RBK) * ld * 8);
+        const BufferSrc<double> src(base, (KC ? BT : RG<BT, UN>::RBK) * ld * 8);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rs, (__attribute__((address_space(3))) void*)(img + ins * 1024),
                                                  16, off, 0, 0, 0);
     } else {
@@ -333,11 +337,11 @@ __device__ __forceinline__ void piece(const double* X, i64 ld, i64 R0, i64 k0, i
     }
 }
 
-template <int BT>
-struct Ops { double a[RG<BT>::MI], b[RG<BT>::MI]; };
+template <int BT, int UN>
+struct Ops { double a[RG<BT, UN>::MI], b[RG<BT, UN>::MI]; };
 // this lane's buffer offsets (bytes) / element offsets of its pieces per operand
-template <int BT>
-struct Pieces { int offA[RG<BT>::NPW], offB[RG<BT>::NPW]; i64 gA[RG<BT>::NPW], gB[RG<BT>::NPW]; };
+template <int BT, int UN>
+struct Pieces { int offA[RG<BT, UN>::NPW], offB[RG<BT, UN>::NPW]; i64 gA[RG<BT, UN>::NPW], gB[RG<BT, UN>::NPW]; };
 
 // acc += a b.  The builtin, not asm: hipcc's hazard recognizer then pads the
 // operand hazards (an asm MFMA here gave wrong products on 1.4 % of the entries:
@@ -351,13 +355,13 @@ __device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
 // one k-step: NM MFMAs on `cur`; the next k-step's NR operand reads (k-step
 // `srd` of the K-tile in rdA / rdB) into `nxt` over the first half of them; NP
 // pieces u0.. of one unit into `st` over the second half
-template <int BT, bool KCA, bool KCB, bool BUF, bool SB, int NP>
+template <int BT, int UN, bool KCA, bool KCB, bool BUF, bool SB, int NP>
 __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, int l, int wr, int wc,
-                                      const Pieces<BT>& pc, const lds_char* __restrict__ rdA,
+                                      const Pieces<BT, UN>& pc, const lds_char* __restrict__ rdA,
                                       const lds_char* __restrict__ rdB, int srd, lds_char* __restrict__ st,
-                                      int u0, i64 k0, f64x4 (&acc)[RG<BT>::MI][RG<BT>::MI], const Ops<BT>& cur,
-                                      Ops<BT>& nxt) {
-    constexpr int MI = RG<BT>::MI, NM = RG<BT>::NM, NR = RG<BT>::NR, WT = RG<BT>::WT, H = NM / 2;
+                                      int u0, i64 k0, f64x4 (&acc)[RG<BT, UN>::MI][RG<BT, UN>::MI], const Ops<BT, UN>& cur,
+                                      Ops<BT, UN>& nxt) {
+    constexpr int MI = RG<BT, UN>::MI, NM = RG<BT, UN>::NM, NR = RG<BT, UN>::NR, WT = RG<BT, UN>::WT, H = NM / 2;
     // BT 128: reads one per MFMA of the first half, pieces SP apart in the second
     // half from its second MFMA on (at 2 pieces); BT 64: two reads per MFMA
     constexpr int RPM = NR / H;
@@ -369,15 +373,15 @@ __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, i
 #pragma unroll
             for (int q = 0; q < RPM; ++q) {
                 const int f = i * RPM + q;
-                if (f < MI) nxt.a[f] = ropnd<BT, KCA>(rdA, wr * WT + f * 16, srd, l);
-                else nxt.b[f - MI] = ropnd<BT, KCB>(rdB, wc * WT + (f - MI) * 16, srd, l);
+                if (f < MI) nxt.a[f] = ropnd<BT, UN, KCA>(rdA, wr * WT + f * 16, srd, l);
+                else nxt.b[f - MI] = ropnd<BT, UN, KCB>(rdB, wc * WT + (f - MI) * 16, srd, l);
             }
         }
         if constexpr (NP > 0) {
             if (i >= H + OFF && (i - H - OFF) % SP == 0 && (i - H - OFF) / SP < NP) {
                 const int u = u0 + (i - H - OFF) / SP;
-                if constexpr (SB) piece<BT, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
-                else piece<BT, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
+                if constexpr (SB) piece<BT, UN, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
+                else piece<BT, UN, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
             }
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the placement as written
@@ -385,10 +389,10 @@ __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, i
 }
 }  // namespace ring
 
-template <int BT, bool KCA, bool KCB, bool BETA0, bool BUF>
-__global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GParams p) {
+template <int BT, int UN, bool KCA, bool KCB, bool BETA0, bool BUF>
+__global__ __launch_bounds__(256, (ring::RG<BT, UN>::MINB)) void gemm_f64r_kernel(GParams p) {
     using namespace ring;
-    using G = RG<BT>;
+    using G = RG<BT, UN>;
     constexpr int RBK = G::RBK, UNIT = G::UNIT, WT = G::WT, MI = G::MI, NKS = G::NKS, NPW = G::NPW;
     constexpr int NPA = NPW / (NKS / 2);  // pieces of A_{t+2} per k-step over the first half
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
@@ -406,11 +410,11 @@ __global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GPar
         p.B += KCB ? kz0 : kz0 * p.ldb;
         p.C += (i64)blockIdx.y * p.zstride;
     }
-    Pieces<BT> pc;
+    Pieces<BT, UN> pc;
 #pragma unroll
     for (int u = 0; u < NPW; ++u) {
-        pc.gA[u] = piece_off<BT, KCA>(w + 4 * u, l, m0, p.m, p.lda);
-        pc.gB[u] = piece_off<BT, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.gA[u] = piece_off<BT, UN, KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<BT, UN, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
         pc.offA[u] = (int)(pc.gA[u] * 8);
         pc.offB[u] = (int)(pc.gB[u] * 8);
     }
@@ -427,18 +431,18 @@ __global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GPar
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int u = 0; u < NPW; ++u)
-            piece<BT, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+            piece<BT, UN, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
 #pragma unroll
         for (int u = 0; u < NPW; ++u)
-            piece<BT, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+            piece<BT, UN, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
     }
     wait_cnt<2 * NPW, NOWAIT_LGKM>();
     dma_barrier();
-    Ops<BT> X, Y;
+    Ops<BT, UN> X, Y;
 #pragma unroll
     for (int q = 0; q < MI; ++q) {
-        X.a[q] = ropnd<BT, KCA>(lds, wr * WT + q * 16, 0, l);
-        X.b[q] = ropnd<BT, KCB>(lds + UNIT, wc * WT + q * 16, 0, l);
+        X.a[q] = ropnd<BT, UN, KCA>(lds, wr * WT + q * 16, 0, l);
+        X.b[q] = ropnd<BT, UN, KCB>(lds + UNIT, wc * WT + q * 16, 0, l);
     }
     wait_cnt<NOWAIT_VM, 0>();
     auto ktile = [&](auto jc, int t) {
@@ -454,10 +458,10 @@ __global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GPar
             constexpr int S = decltype(sc)::value;
             constexpr int NP = S < NKS / 2 ? NPA : 0;
             if constexpr (S % 2 == 0)
-                ring::kstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
+                ring::kstep<BT, UN, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
                                                           lds + st0 * UNIT, S * NPA, k2, acc, X, Y);
             else
-                ring::kstep<BT, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
+                ring::kstep<BT, UN, KCA, KCB, BUF, false, NP>(p, m0, n0, w, l, wr, wc, pc, rA, rB, S + 1,
                                                           lds + st0 * UNIT, S * NPA, k2, acc, Y, X);
             if constexpr (S < NKS - 2) wait_cnt<NOWAIT_VM, 0>();
         };
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(256, ring::RG<BT>::MINB) void gemm_f64r_kernel(GPar
         wait_cnt<NPW, 0>();  // A_{t+1}, B_{t+1} landed (A_{t+2} may fly); reads of A_t, B_t retired
         dma_barrier();
         // (t,NKS-1): operands of (t+1,0) from A_{t+1}, B_{t+1}; B_{t+2} into A_t's slot
-        ring::kstep<BT, KCA, KCB, BUF, true, NPW>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT,
+        ring::kstep<BT, UN, KCA, KCB, BUF, true, NPW>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT,
                                                   0, lds + st1 * UNIT, 0, k2, acc, Y, X);
         wait_cnt<NOWAIT_VM, 0>();
     };
@@ -551,19 +555,19 @@ hipError_t launch_g(GParams p, hipStream_t s) {
     return launch_b<SH, KCA, KCB, false>(p, grid, s);
 }
 
-template <int BT, bool KCA, bool KCB>
+template <int BT, int UN, bool KCA, bool KCB>
 hipError_t launch_r(GParams p, hipStream_t s) {
-    constexpr int RBK = ring::RG<BT>::RBK;
+    constexpr int RBK = ring::RG<BT, UN>::RBK;
     p.tiles_m = (int)((p.m + BT - 1) / BT);
     p.tiles_n = (int)((p.n + BT - 1) / BT);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
     const bool buf = dma_fits(KCA ? BT : RBK, p.lda, 8) && dma_fits(KCB ? BT : RBK, p.ldb, 8);
     if (p.beta == 0.0) {
-        if (buf) return launch(gemm_f64r_kernel<BT, KCA, KCB, true, true>, grid, 256, p, s);
-        return launch(gemm_f64r_kernel<BT, KCA, KCB, true, false>, grid, 256, p, s);
+        if (buf) return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, true, true>, grid, 256, p, s);
+        return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, true, false>, grid, 256, p, s);
     }
-    if (buf) return launch(gemm_f64r_kernel<BT, KCA, KCB, false, true>, grid, 256, p, s);
-    return launch(gemm_f64r_kernel<BT, KCA, KCB, false, false>, grid, 256, p, s);
+    if (buf) return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, false, true>, grid, 256, p, s);
+    return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, false, false>, grid, 256, p, s);
 }
 
 template <typename SH>
@@ -635,12 +639,12 @@ hipError_t gemm_f64_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
     static const int t64w = [] { const char* v = getenv("ELX_F64G_T64W"); return v ? atoi(v) : 0; }();
     const int bt = ring_bt(m, n, kmain);
     if (bt == 128 && kmain % 32 == 0 && kchunk % 32 == 0) {
-        if (ta) return !tb ? launch_r<128, true, true>(p, s) : launch_r<128, true, false>(p, s);
-        return !tb ? launch_r<128, false, true>(p, s) : launch_r<128, false, false>(p, s);
+        if (ta) return !tb ? launch_r<128, 32768, true, true>(p, s) : launch_r<128, 32768, true, false>(p, s);
+        return !tb ? launch_r<128, 32768, false, true>(p, s) : launch_r<128, 32768, false, false>(p, s);
     }
     if (bt == 64 && kmain % 16 == 0 && kchunk % 16 == 0) {
-        if (ta) return !tb ? launch_r<64, true, true>(p, s) : launch_r<64, true, false>(p, s);
-        return !tb ? launch_r<64, false, true>(p, s) : launch_r<64, false, false>(p, s);
+        if (ta) return !tb ? launch_r<64, 8192, true, true>(p, s) : launch_r<64, 8192, true, false>(p, s);
+        return !tb ? launch_r<64, 8192, false, true>(p, s) : launch_r<64, 8192, false, false>(p, s);
     }
     if (t64_tiles(m, n, kmain)) {
         if (t64w == 8 || (t64w != 4 && !ta)) return launch_shape<Shape<64, 32, BK, 64, 16>>(ta, !tb, p, s);
