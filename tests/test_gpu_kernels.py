@@ -161,7 +161,7 @@ def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
     (r, sh, b) for r in ("1", "0") for sh, b in [((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0),
                                                  ((2048, 4096, 2072), -1.0), ((4096, 2048, 32), 0.5)]] + [
     ("2", (1536, 2048, 640), -1.0), ("2", (1000, 1016, 1056), 0.0), ("2", (1536, 2048, 2072), -1.0),
-    ("2", (1024, 512, 16), 0.5)])
+    ("2", (1024, 512, 16), 0.5), ("2", (512, 512, 2048), -1.0), ("2", (520, 600, 3000), 0.0)])
 def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     """The fp64 ring kernel (gemm_f64r_kernel: four waves, a 5-slot LDS ring of
     32-deep K-tiles; ELX_F64G_RING=1) on 128-tile grids: many wraps of the ring
@@ -171,8 +171,9 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     Integer operands: exact in every orientation.  ring = "0": the same cases
     through the two-stage slab kernel it replaced as the default; ring = "2":
     the 64 x 64 ring (16-deep K-tiles, four workgroups per CU) on grids of
-    64-tiles, likewise with a ragged grid, a k tail (2072 = 129 x 16 + 8) and a
-    single K-tile."""
+    64-tiles, likewise with a ragged grid, a k tail (2072 = 129 x 16 + 8), a
+    single K-tile, and grids of 64 / 90 tiles that split k into chunks
+    (partials through splitk_reduce)."""
     monkeypatch.setenv("ELX_F64G_RING", ring)
     m, n, k = shape
     rng = np.random.default_rng(m + k)
@@ -202,7 +203,7 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     ("2", (1024, 1024, 2048), -1.0), ("2", (1000, 1016, 1152), 0.0), ("2", (1536, 2048, 2100), -1.0),
     ("2", (1024, 512, 128), 0.5),
     ("4", (1536, 2048, 640), -1.0), ("4", (1000, 1016, 1056), 0.0), ("4", (1536, 2048, 2100), -1.0),
-    ("4", (1024, 512, 32), 0.5),
+    ("4", (1024, 512, 32), 0.5), ("4", (512, 512, 4096), -1.0), ("4", (520, 600, 3000), 0.0),
     ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)])
 def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
     """The fp32 ring kernel (gemm_f32r_kernel; ELX_F32G_RING bit 0: 128 x 128
@@ -212,7 +213,8 @@ def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
     through the general kernel (2072 = 32 x 64 + 24, 2100 = 16 x 128 + 52), a
     single K-tile (prologue and clamped restaging only), and the k-permuted
     MFMA steps in every orientation.  ring = "4": the 64 x 64 ring with 32-deep
-    K-tiles and four workgroups per CU, likewise (2100 = 65 x 32 + 20).  ring =
+    K-tiles and four workgroups per CU, likewise (2100 = 65 x 32 + 20), and on
+    grids small enough to split k into chunks.  ring =
     "0": the slab kernels on the ragged cases.  Integer operands: exact."""
     monkeypatch.setenv("ELX_F32G_RING", ring)
     m, n, k = shape
