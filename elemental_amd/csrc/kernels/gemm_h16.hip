@@ -432,7 +432,9 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 // PART: split-k partials (p.W, gridDim.y chunks), a separate instantiation so the
 // default kernel's epilogue keeps its register allocation.  WM = 8: one
 // workgroup per CU (the whole register file and LDS); WM = 4: two.
-template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART>
+// SWP: B is the operand of the even units (staged first in a K-tile, one k-step
+// more DMA lead), A of the odd ones.
+template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART, bool SWP = false>
 __global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
     constexpr int BMR = Geo<WM>::BM, UNIT = Geo<WM>::UNIT;
@@ -472,22 +474,30 @@ __global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params
     const int nt = (int)(p.k / BK);
     auto kt = [&](int t) { return (i64)min(t, nt - 1) * BK; };
     // prologue: A_0, B_0, A_1, B_1 into slots 0..3; wait for A_0, B_0; fragments (0,0)
+    constexpr int OA = SWP ? 1 : 0, OB = SWP ? 0 : 1;  // unit parity of A / B
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+        if constexpr (SWP) {
+#pragma unroll
+            for (int u = 0; u < WM; ++u)
+                piece<BMR, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + OB) * UNIT);
+        }
 #pragma unroll
         for (int u = 0; u < WM; ++u)
-            piece<BMR, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + 2 * t * UNIT);
+            piece<BMR, BUF, KCA>(p.A, p.lda, m0, kt(t), pc.offA[u], pc.gA[u], w + 4 * u, lds + (2 * t + OA) * UNIT);
+        if constexpr (!SWP) {
 #pragma unroll
-        for (int u = 0; u < WM; ++u)
-            piece<BMR, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + 1) * UNIT);
+            for (int u = 0; u < WM; ++u)
+                piece<BMR, BUF, KCB>(p.B, p.ldb, n0, kt(t), pc.offB[u], pc.gB[u], w + 4 * u, lds + (2 * t + OB) * UNIT);
+        }
     }
     wait_cnt<2 * WM, NOWAIT_LGKM>();
     bar8();
     Sets<WM> X, Y;
 #pragma unroll
     for (int q = 0; q < WM; ++q) {
-        X.a[q] = wfrag<WM, KCA>(lds, wr, q, 0, l);
-        X.b[q] = wfrag<WM, KCB>(lds + UNIT, wc, q, 0, l);
+        X.a[q] = wfrag<WM, KCA>(lds + OA * UNIT, wr, q, 0, l);
+        X.b[q] = wfrag<WM, KCB>(lds + OB * UNIT, wc, q, 0, l);
     }
     wait_cnt<NOWAIT_VM, 0>();
     // One K-tile; J = t % 5 makes every slot a compile-time offset of the LDS
@@ -495,15 +505,16 @@ __global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params
     // the DMA destinations need no address arithmetic in the loop.
     auto ktile = [&](auto jc, int t) {
         constexpr int J = decltype(jc)::value;
-        constexpr int sA = 2 * J % NSLOT, sB = (2 * J + 1) % NSLOT, sA1 = (2 * J + 2) % NSLOT,
-                      sB1 = (2 * J + 3) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
-        // (t,0): stage A_{t+2} into B_{t-1}'s slot
-        w4::kstep<WM, BF16, KCA, KCB, BUF, false>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
-                                                     lds + st0 * UNIT, kt(t + 2), acc, X, Y);
+        constexpr int sA = (2 * J + OA) % NSLOT, sB = (2 * J + OB) % NSLOT, sA1 = (2 * J + 2 + OA) % NSLOT,
+                      sB1 = (2 * J + 2 + OB) % NSLOT, st0 = (2 * J + 4) % NSLOT, st1 = (2 * J + 5) % NSLOT;
+        // (t,0): stage the even unit of t+2 (A_{t+2}; B_{t+2} if SWP) into the odd
+        // unit of t-1's slot
+        w4::kstep<WM, BF16, KCA, KCB, BUF, SWP>(p, m0, n0, w, l, wr, wc, pc, lds + sA * UNIT, lds + sB * UNIT, 1,
+                                                   lds + st0 * UNIT, kt(t + 2), acc, X, Y);
         wait_cnt<WM, 0>();
         bar8();
-        // (t,1): stage B_{t+2} into A_t's slot
-        w4::kstep<WM, BF16, KCA, KCB, BUF, true>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
+        // (t,1): stage the odd unit of t+2 into the even unit of t's slot
+        w4::kstep<WM, BF16, KCA, KCB, BUF, !SWP>(p, m0, n0, w, l, wr, wc, pc, lds + sA1 * UNIT, lds + sB1 * UNIT, 0,
                                                     lds + st1 * UNIT, kt(t + 2), acc, Y, X);
         wait_cnt<NOWAIT_VM, 0>();
     };
@@ -532,9 +543,19 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
     // global (64-bit address) form
     const bool buf = dma_fits(KCA ? BMR : BK, p.lda, 2) && dma_fits(KCB ? BMR : BK, p.ldb, 2);
     const dim3 grid(p.tiles_m * p.tiles_n, p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
+    // B's units first (SWP) except for NN, 256 x 256 tiles: one process, bf16
+    // 16384^3 NN / NT / TN / TT 1523 / 1421 / 1514 / 1428 -> 1494 / 1459 / 1529 /
+    // 1509 TF with B first, 32768^3 NN 1451 -> 1432, TT 1379 -> 1440
+    // (profiles/r05as_h16_swap_ab.log): the operand whose misses land later (a
+    // rows-contiguous B, or B when the two are alike) gets the longer DMA lead.
+    // ELX_H16_SWAP = 0 / 1 forces (read per call, A/B and tests).
+    const char* sw = getenv("ELX_H16_SWAP");
+    const bool swp = sw ? sw[0] == '1' : (WM == 8 && (KCA || !KCB));
     if (p.W) {
         if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, true, true>), grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, false, true>), grid, dim3(256), 0, s, p);
+    } else if (swp && buf) {
+        hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, true, false, true>), grid, dim3(256), 0, s, p);
     } else {
         if (buf) hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, true, false>), grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL((gemm_h4w_kernel<WM, BF16, KCA, KCB, false, false>), grid, dim3(256), 0, s, p);
