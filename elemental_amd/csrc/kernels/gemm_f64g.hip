@@ -368,7 +368,7 @@ __device__ __forceinline__ void kstep(const GParams& p, i64 m0, i64 n0, int w, i
     constexpr int SP = NP > 0 ? H / NP : 1, OFF = (SP > 1 && BT == 128) ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
-        mfma_acc(acc[i / MI][i % MI], cur.a[i / MI], cur.b[i % MI]);
+        mfma_acc(acc[i / MI][i % MI], cur.b[i % MI], cur.a[i / MI]);  // D^T: C rows across lanes
         if (i < H) {
 #pragma unroll
             for (int q = 0; q < RPM; ++q) {
@@ -490,9 +490,13 @@ __global__ __launch_bounds__(256, (ring::RG<BT, UN>::MINB)) void gemm_f64r_kerne
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
 
-    // Epilogue: C/D map of v_mfma_f64_16x16x4_f64: row = (lane>>4) + 4*reg, col = lane&15
+    // Epilogue: the MFMAs computed (op(A) op(B))^T blocks (B fragments as the
+    // first operand), so lane l, register r of accumulator (mi, ni) holds C row
+    // mi*16 + (l & 15), column ni*16 + (l >> 4) + 4 r: 16 lanes write 128
+    // contiguous bytes of a column (v_mfma_f64_16x16x4_f64's D map is row =
+    // (lane>>4) + 4 reg, col = lane & 15)
     const int g = l >> 4, c = l & 15;
-    const i64 ib = m0 + wr * WT, jb = n0 + wc * WT;
+    const i64 ib = m0 + wr * WT + c, jb = n0 + wc * WT + g;
     if (m0 + BT <= p.m && n0 + BT <= p.n) {
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) {
@@ -501,14 +505,14 @@ __global__ __launch_bounds__(256, (ring::RG<BT, UN>::MINB)) void gemm_f64r_kerne
 #pragma unroll
                 for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r];
+                    for (int r = 0; r < 4; ++r) cv[ni][r] = p.C[(jb + ni * 16 + 4 * r) * p.ldc + ib + mi * 16];
             }
 #pragma unroll
             for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const double v = p.alpha * acc[mi][ni][r];
-                    p.C[(jb + ni * 16 + c) * p.ldc + ib + mi * 16 + g + 4 * r] = BETA0 ? v : v + p.beta * cv[ni][r];
+                    p.C[(jb + ni * 16 + 4 * r) * p.ldc + ib + mi * 16] = BETA0 ? v : v + p.beta * cv[ni][r];
                 }
         }
         return;
@@ -517,15 +521,15 @@ __global__ __launch_bounds__(256, (ring::RG<BT, UN>::MINB)) void gemm_f64r_kerne
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < MI; ++ni) {
-            const i64 j = jb + ni * 16 + c;
-            if (j >= p.n) continue;
-            double* col = p.C + j * p.ldc;
+            const i64 i = ib + mi * 16;
+            if (i >= p.m) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const i64 i = ib + mi * 16 + g + 4 * r;
-                if (i < p.m) {
+                const i64 j = jb + ni * 16 + 4 * r;
+                if (j < p.n) {
                     const double v = p.alpha * acc[mi][ni][r];
-                    col[i] = BETA0 ? v : v + p.beta * col[i];
+                    double* cp = p.C + j * p.ldc + i;
+                    *cp = BETA0 ? v : v + p.beta * *cp;
                 }
             }
         }
