@@ -8,7 +8,9 @@ peer) injected on the library's high-priority comm stream every `gap_ms`
 while it runs.  Reported: the GEMM time alone and with the copies, and each
 copy's event-timed duration alone and under the GEMM (a copy whose workgroups
 cannot find a CU waits for GEMM workgroups to retire).  Run once per
-ELX_COMM_CUS setting (CUs masked off the compute stream, read at init):
+ELX_COMM_CUS setting (CUs masked off the compute stream, read at init);
+OVERLAP_OP=sum injects a reduction instead (workgroups that need LDS, as RCCL's
+kernels do, beside a GEMM whose ring kernel holds every CU's LDS):
 
   ELX_COMM_CUS=0 python tools/overlap_probe.py ; ELX_COMM_CUS=8 python tools/overlap_probe.py
 """
@@ -42,6 +44,8 @@ def main():
     mstream = torch.cuda.ExternalStream(mp.value)
     src = torch.rand(copy_mib * (1 << 20) // 8, dtype=torch.float64, device="cuda")
     dst = torch.empty_like(src)
+    red = torch.empty((), dtype=torch.float64, device="cuda")
+    op = os.environ.get("OVERLAP_OP", "copy")
     torch.cuda.synchronize()
 
     def gemm_ms():
@@ -55,7 +59,10 @@ def main():
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(mstream):
             a.record(mstream)
-            dst.copy_(src)
+            if op == "sum":  # a reduction: workgroups that need LDS, as RCCL's kernels do
+                torch.sum(src, dim=0, out=red)
+            else:
+                dst.copy_(src)
             b.record(mstream)
         return a, b
 
@@ -87,6 +94,7 @@ def main():
         "gemm_ms_with_copies": round(gemm_with, 2),
         "gemm_slowdown": round(gemm_with / gemm_alone, 4),
         "gemm_tflops_alone": round(2 * n ** 3 / (gemm_alone * 1e-3) / 1e12, 2),
+        "injected": "torch.sum (LDS-using reduction)" if op == "sum" else "device copy",
         "copy_mib": copy_mib,
         "copy_ms_alone_median": round(copy_alone[len(copy_alone) // 2], 3),
         "copy_GBps_alone_median": gbs(copy_alone[len(copy_alone) // 2]),
