@@ -565,7 +565,12 @@ hipError_t launch_r(GParams p, hipStream_t s) {
     p.tiles_m = (int)((p.m + BT - 1) / BT);
     p.tiles_n = (int)((p.n + BT - 1) / BT);
     const dim3 grid(p.tiles_m * p.tiles_n, (unsigned)((p.k + p.kchunk - 1) / p.kchunk));
-    const bool buf = dma_fits(KCA ? BT : RBK, p.lda, 8) && dma_fits(KCB ? BT : RBK, p.ldb, 8);
+    // buffer-descriptor DMA when every offset of an image fits 31 bits, else the
+    // global (64-bit address) form; ELX_F64G_STAGE=g forces the latter (read per call:
+    // the tests cover it without operands of 2^21+ elements per row)
+    const char* stg = getenv("ELX_F64G_STAGE");
+    const bool buf = !(stg && stg[0] == 'g') && dma_fits(KCA ? BT : RBK, p.lda, 8) &&
+                     dma_fits(KCB ? BT : RBK, p.ldb, 8);
     if (p.beta == 0.0) {
         if (buf) return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, true, true>, grid, 256, p, s);
         return launch(gemm_f64r_kernel<BT, UN, KCA, KCB, true, false>, grid, 256, p, s);

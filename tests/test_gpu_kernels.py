@@ -162,7 +162,8 @@ def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
                                                  ((2048, 4096, 2072), -1.0), ((4096, 2048, 32), 0.5)]] + [
     ("2", (1536, 2048, 640), -1.0), ("2", (1000, 1016, 1056), 0.0), ("2", (1536, 2048, 2072), -1.0),
     ("2", (1024, 512, 16), 0.5), ("2", (512, 512, 2048), -1.0), ("2", (520, 600, 3000), 0.0)])
-def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
+@pytest.mark.parametrize("stage", ["buf", "global"])
+def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, stage, monkeypatch):
     """The fp64 ring kernel (gemm_f64r_kernel: four waves, a 5-slot LDS ring of
     32-deep K-tiles; ELX_F64G_RING=1) on 128-tile grids: many wraps of the ring
     (k = 640: 20 K-tiles), ragged edge tiles with beta = 0 (C holds NaN and must
@@ -175,6 +176,10 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     single K-tile, and grids of 64 / 90 tiles that split k into chunks
     (partials through splitk_reduce)."""
     monkeypatch.setenv("ELX_F64G_RING", ring)
+    if stage == "global":  # the 64-bit-address DMA form (operands too long for 31-bit offsets)
+        if ring == "0":
+            pytest.skip("the slab kernels read ELX_F64G_STAGE once per process")
+        monkeypatch.setenv("ELX_F64G_STAGE", "g")
     m, n, k = shape
     rng = np.random.default_rng(m + k)
     A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float64))
@@ -205,7 +210,8 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, monkeypatch):
     ("4", (1536, 2048, 640), -1.0), ("4", (1000, 1016, 1056), 0.0), ("4", (1536, 2048, 2100), -1.0),
     ("4", (1024, 512, 32), 0.5), ("4", (512, 512, 4096), -1.0), ("4", (520, 600, 3000), 0.0),
     ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)])
-def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
+@pytest.mark.parametrize("stage", ["buf", "global"])
+def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, stage, monkeypatch):
     """The fp32 ring kernel (gemm_f32r_kernel; ELX_F32G_RING bit 0: 128 x 128
     tiles with 64-deep K-tiles on grids of 128-tiles, bit 1: 64 x 64 tiles with
     128-deep K-tiles on grids of 64-tiles): many wraps of the 5-slot ring, ragged
@@ -217,6 +223,10 @@ def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, monkeypatch):
     grids small enough to split k into chunks.  ring =
     "0": the slab kernels on the ragged cases.  Integer operands: exact."""
     monkeypatch.setenv("ELX_F32G_RING", ring)
+    if stage == "global":  # the 64-bit-address DMA form (operands too long for 31-bit offsets)
+        if ring == "0":
+            pytest.skip("the slab kernels read ELX_F32G_STAGE once per process")
+        monkeypatch.setenv("ELX_F32G_STAGE", "g")
     m, n, k = shape
     rng = np.random.default_rng(m + k + 1)
     A = np.asfortranarray(rng.integers(-4, 4, (m, k) if ta == "N" else (k, m)).astype(np.float32))
