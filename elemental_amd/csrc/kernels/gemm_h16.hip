@@ -541,7 +541,9 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
     constexpr int BMR = w4::Geo<WM>::BM;
     // buffer-descriptor DMA when every offset of an image fits 31 bits, else the
     // global (64-bit address) form
-    const bool buf = dma_fits(KCA ? BMR : BK, p.lda, 2) && dma_fits(KCB ? BMR : BK, p.ldb, 2);
+    // (ELX_H16_STAGE=g, read per call, forces the global form: the tests cover it)
+    const char* stg = getenv("ELX_H16_STAGE");
+    const bool buf = !(stg && stg[0] == 'g') && dma_fits(KCA ? BMR : BK, p.lda, 2) && dma_fits(KCB ? BMR : BK, p.ldb, 2);
     const dim3 grid(p.tiles_m * p.tiles_n, p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
     // B's units first (SWP) except for NN, 256 x 256 tiles: one process, bf16
     // 16384^3 NN / NT / TN / TT 1523 / 1421 / 1514 / 1428 -> 1494 / 1459 / 1529 /

@@ -314,7 +314,7 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
     assert bad.size == 0, f"{kind} alpha={alpha} beta={beta}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
-@pytest.mark.parametrize("tile", ["", "128", "256"])
+@pytest.mark.parametrize("tile", ["", "128", "256", "g"])
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
@@ -335,8 +335,12 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     128 x 128 / 256 x 256 (ELX_H16_TILE), so both instantiations see every
     shape.  (4096, 4096, 192): a 16 x 16 grid of 256-tiles, run in the
     super-block tile order (tile_of_sb).  (k a multiple of 64: a k tail is a
-    second pass that adds to the already rounded C.)"""
-    if tile:
+    second pass that adds to the already rounded C.)  tile = "g": the plan's
+    tile with the DMA in its 64-bit-address form (ELX_H16_STAGE=g; operands too
+    long for 31-bit buffer offsets take it)."""
+    if tile == "g":
+        monkeypatch.setenv("ELX_H16_STAGE", "g")
+    elif tile:
         monkeypatch.setenv("ELX_H16_TILE", tile)
     m, n, k = shape
     rng = np.random.default_rng(m + n + k)
