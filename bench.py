@@ -2,8 +2,10 @@
 """Headline benchmark: distributed El::Gemm TFLOP/s on MI355X (BASELINE.json metric).
 
   python bench.py --gpus N --steps K --warmup W [--config c2|c3|c4|c5]
-  (N > 1: launched by torch.distributed.run, one process per GPU; RANK /
-   LOCAL_RANK / WORLD_SIZE / MASTER_* come from the environment)
+  (N > 1: one process per GPU.  Under torch.distributed.run RANK / LOCAL_RANK /
+   WORLD_SIZE / MASTER_* come from the environment; with WORLD_SIZE unset this
+   script starts the N rank processes itself with that same environment
+   (launch_ranks) and exits with the first failing rank's status)
 
 One step = one El::Gemm(...) on DistMatrix operands already resident in HBM,
 inputs from the grid-independent counter hash (synthetic data, Uniform(-0.1,
@@ -20,6 +22,8 @@ Default workload (the driver's line):
   N > 1 first checks the reference's associativity residual through the
           distributed path (n = 4096) and reports xGMI GB/s from transfer-only
           events plus the compute-stream gaps the panel pipeline left exposed.
+  N > 1 runs C3 and the residual only (--extra-configs adds the C4 / C5 points
+          after it).
 Extra lines (evidence, not the driver's default):
   --config c4 : TN fp32 m=n=8192, k=524288*N, inputs [VC,STAR] (LBANN's
                 weight-gradient shape, SUMMA_DOT); weak scaling, = C4 at N=8.
@@ -340,7 +344,101 @@ def config_point(el, L, grid, barrier, maxr, config: str, steps: int, warmup: in
     return out
 
 
+def _free_port() -> int:
+    """A loopback port that is free now, with port + 1 free too (the library's own
+    rendezvous defaults to MASTER_PORT + 1, comm.cpp InitWorldFromEnv), drawn below
+    the ephemeral range so no outgoing connection can take it meanwhile."""
+    import random
+    import socket
+    for _ in range(256):
+        port = random.randrange(20000, 32000)
+        try:
+            with socket.socket() as s, socket.socket() as s2:
+                s.bind(("127.0.0.1", port))
+                s2.bind(("127.0.0.1", port + 1))
+            return port
+        except OSError:
+            continue
+    raise RuntimeError("no free loopback port pair in 20000-32000")
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    """The environment torch.distributed.run gives rank `rank` of a one-node job:
+    the launcher variables the reference maps to a device
+    (src/hydrogen/device/GPU.cpp:30-50: LOCAL_RANK picks the GPU)."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", ROLE_RANK=str(rank), ROLE_WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+    return env
+
+
+def launch_ranks(argv: list[str], world: int, child_cmd: list[str] | None = None, grace_s: float = 45.0,
+                 poll_s: float = 0.2) -> int:
+    """`python3 bench.py --gpus N` with no launcher around it (WORLD_SIZE unset):
+    start N child processes of this script, one per GPU, with the environment
+    torch.distributed.run would give them (rank_env), and wait.  Called before
+    torch or the library is imported, so this process never touches the GPU and
+    never execs.  Children inherit stdout, so rank 0's JSON line is the line the
+    caller reads.  Exit status: 0 when every rank exits 0; otherwise the first
+    failing rank's status (a signal death maps to 128 + signal).  After the first
+    failure the others get `grace_s` to end on their own (their watchdog aborts
+    RCCL and exits naming the stage), then SIGTERM, then SIGKILL -- by PID, only
+    the processes started here.  SIGTERM / SIGINT to this process are forwarded."""
+    import signal
+    import subprocess
+    port = _free_port()
+    cmd = child_cmd or [sys.executable, "-u", os.path.abspath(__file__)]
+    procs = [subprocess.Popen(cmd + list(argv), env=rank_env(os.environ, r, world, port)) for r in range(world)]
+
+    def stop_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all(signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    status = 0
+    failed_at = None
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            for r, c in enumerate(codes):
+                if c is not None and c != 0 and status == 0:
+                    status = c if c > 0 else 128 - c
+                    failed_at = time.monotonic()
+                    print(f"[bench launcher] rank {r} exited with status {c}; "
+                          f"stopping the others in {grace_s:.0f} s", file=sys.stderr, flush=True)
+            if all(c is not None for c in codes):
+                break
+            if failed_at is not None:
+                waited = time.monotonic() - failed_at
+                if waited > grace_s + 10:
+                    stop_all(signal.SIGKILL)
+                elif waited > grace_s:
+                    stop_all(signal.SIGTERM)
+            time.sleep(poll_s)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return status
+
+
 def main():
+    # N > 1 without a launcher: become the launcher (decided before torch or the
+    # library is loaded; this process never initialises the GPU)
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        n, _ = pre.parse_known_args()
+        if n.gpus > 1:
+            sys.exit(launch_ranks(sys.argv[1:], n.gpus))
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -358,7 +456,19 @@ def main():
                     help="N=1: skip the same-problem C3 point (n=65536 through the panel path)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="N=1: skip the C4 / C5 single-GPU points of the default line")
+    ap.add_argument("--extra-configs", action="store_true",
+                    help="N>1: also run the C4 / C5 points after C3 (off by default, so an "
+                         "overrun there cannot touch the C3 line; --config c4 / c5 print them alone)")
     args = ap.parse_args()
+
+    # stdout carries exactly one line, the JSON: whatever the libraries print on
+    # file descriptor 1 (gloo's "[Gloo] Rank ... connected" lines, RCCL's INFO
+    # output) goes to stderr from here on, and the line goes out through a
+    # duplicate of the original descriptor
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    os.environ["ELX_WATCHDOG_FD"] = str(line_out.fileno())  # the watchdog's epitaph line goes there too
 
     import torch
     from elemental_amd import el
@@ -599,9 +709,11 @@ def main():
         extra("c3_1gpu", lambda: c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc))
         # C3 is "fp64/fp32": the fp32 half of the same problem
         extra("c3_1gpu_f32", lambda: c3_one_gpu(el, L, grid, barrier, args.c3_steps, 1, args.kc, dtype="f32"))
-    if config in ("c2", "c3") and (not args.n or rehearse) and not args.no_extra_configs:
+    extras = (world == 1 and not args.no_extra_configs) or (world > 1 and args.extra_configs)
+    if config in ("c2", "c3") and (not args.n or rehearse) and extras:
         # the other BASELINE configs, measured in the same run on the same grid
-        # (N = 1: c4_1gpu / c5_1gpu; N > 1: c4 / c5 on Grid::DefaultHeight(N))
+        # (N = 1: c4_1gpu / c5_1gpu; N > 1 with --extra-configs: c4 / c5 on
+        # Grid::DefaultHeight(N))
         A = B = C = None  # release the main operands (no-op when already released)
         # C5 is "bf16/half": both 16-bit types
         for cfg, st, half in (("c4", 2, "bf16"), ("c5", 5, "bf16"), ("c5", 5, "f16")):
@@ -635,7 +747,7 @@ def main():
         extra("cpu_baseline", cpu)
     stage("report", 300)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=line_out, flush=True)
     el.watchdog_epitaph("", 0)
     if dist is not None:
         dist.barrier()

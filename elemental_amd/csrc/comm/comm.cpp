@@ -77,7 +77,10 @@ struct Watchdog {
     double budget = 0;
     std::vector<ncclComm_t> comms;
     bool started = false;
-    std::string epitaph;  // written to stdout before exiting (e.g. a result line already measured)
+    // written to stdout before exiting (e.g. a result line already measured);
+    // to file descriptor ELX_WATCHDOG_FD instead when that is set (a caller that
+    // moved descriptor 1 to stderr keeps its result line on a duplicate)
+    std::string epitaph;
     int epitaph_code = kWatchdogExit;
 
     [[noreturn]] void Fail(const std::string& why) {
@@ -86,7 +89,11 @@ struct Watchdog {
                      stage.c_str(), why.c_str(), comms.size(), code);
         std::fflush(stderr);
         for (ncclComm_t c : comms) (void)ncclCommAbort(c);
-        if (!epitaph.empty()) std::fprintf(stdout, "%s\n", epitaph.c_str());
+        const char* fdv = std::getenv("ELX_WATCHDOG_FD");
+        if (!epitaph.empty()) {
+            if (fdv && *fdv) ::dprintf(std::atoi(fdv), "%s\n", epitaph.c_str());
+            else std::fprintf(stdout, "%s\n", epitaph.c_str());
+        }
         std::fflush(stdout);
         _exit(code);
     }
@@ -720,17 +727,30 @@ struct Fd {
 };
 }  // namespace
 
-// Handshake: each client sends kRdvMagic, its rank and the world size; rank 0
-// serves each valid rank in 1..size-1 once and drops anything else (a stray
-// connection never uses up a peer's slot, and the id is sent only to peers
-// that name this rendezvous).  Rank 0 listens on INADDR_ANY; the peers dial
-// MASTER_ADDR.
+// Handshake: each client sends kRdvMagic, its rank, the world size and the
+// job's token; rank 0 serves each valid rank in 1..size-1 once and drops
+// anything else (a stray or foreign connection never uses up a peer's slot,
+// and the id is sent only to peers that name this rendezvous and this job).
+// The token is a 64-bit FNV-1a hash of ELX_RENDEZVOUS_SECRET, which every rank
+// of a job shares (unset: 0).  Rank 0 listens on MASTER_ADDR itself when that
+// is 127.0.0.1 or a non-loopback address of this host; on every interface only
+// when MASTER_ADDR resolves to another loopback alias (Debian maps the host's
+// own name to 127.0.1.1 while peers on other nodes dial the real address) or
+// the address is not local (EADDRNOTAVAIL).  The peers dial MASTER_ADDR.
 namespace {
-constexpr char kRdvMagic[8] = {'E', 'L', 'X', 'R', 'D', 'V', '0', '1'};
+constexpr char kRdvMagic[8] = {'E', 'L', 'X', 'R', 'D', 'V', '0', '2'};
 struct RdvHello {
     char magic[8];
     int32_t rank, size;
+    uint64_t token;
 };
+uint64_t RdvToken() {
+    const char* s = std::getenv("ELX_RENDEZVOUS_SECRET");
+    if (!s || !*s) return 0;
+    uint64_t h = 14695981039346656037ull;
+    for (; *s; ++s) h = (h ^ static_cast<unsigned char>(*s)) * 1099511628211ull;
+    return h;
+}
 bool ResolveV4(const char* addr, int port, sockaddr_in& out) {
     addrinfo hints{}, *res = nullptr;
     hints.ai_family = AF_INET;
@@ -741,6 +761,19 @@ bool ResolveV4(const char* addr, int port, sockaddr_in& out) {
     ::freeaddrinfo(res);
     return true;
 }
+// bind rank 0's listener (policy above)
+void BindListener(int fd, const sockaddr_in& sa, int port) {
+    const uint32_t ip = ntohl(sa.sin_addr.s_addr);
+    const bool loopback = (ip >> 24) == 127;
+    sockaddr_in at = sa;
+    if (loopback && ip != 0x7F000001u) at.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (::bind(fd, reinterpret_cast<const sockaddr*>(&at), sizeof(at)) == 0) return;
+    if (errno == EADDRNOTAVAIL && at.sin_addr.s_addr != htonl(INADDR_ANY)) {
+        at.sin_addr.s_addr = htonl(INADDR_ANY);
+        if (::bind(fd, reinterpret_cast<const sockaddr*>(&at), sizeof(at)) == 0) return;
+    }
+    throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
+}
 }  // namespace
 
 void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* addr, int port, double timeout_s) {
@@ -748,6 +781,7 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
     ELX_REQUIRE(port > 0 && port < 65536, "rendezvous: bad port ", port);
     if (size == 1) return;
     const double deadline = Now() + timeout_s;
+    const uint64_t token = RdvToken();
     sockaddr_in sa{};
     if (!ResolveV4(addr, port, sa)) throw CommError(Cat("rendezvous: cannot resolve ", addr ? addr : "(null)"));
     if (rank == 0) {
@@ -756,14 +790,8 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
         if (ls.fd < 0) throw CommError("rendezvous: socket() failed");
         const int one = 1;
         ::setsockopt(ls.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-        // Listen on every interface: MASTER_ADDR may resolve to a loopback alias
-        // here (Debian hosts map their own name to 127.0.1.1) while the other
-        // nodes reach the real address.  The handshake rejects stray connections.
-        sockaddr_in any = sa;
-        any.sin_addr.s_addr = htonl(INADDR_ANY);
-        if (::bind(ls.fd, reinterpret_cast<sockaddr*>(&any), sizeof(any)) != 0)
-            throw CommError(Cat("rendezvous: bind to port ", port, " failed: ", std::strerror(errno)));
-        if (::listen(ls.fd, size) != 0) throw CommError("rendezvous: listen() failed");
+        BindListener(ls.fd, sa, port);
+        if (::listen(ls.fd, std::max(size, 128)) != 0) throw CommError("rendezvous: listen() failed");
         std::vector<bool> served(size, false);
         int left = size - 1;
         while (left > 0) {
@@ -781,7 +809,7 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
                 continue;  // silent or short: not a peer
             }
             if (std::memcmp(h.magic, kRdvMagic, sizeof(kRdvMagic)) != 0 || h.size != size || h.rank < 1 ||
-                h.rank >= size || served[h.rank])
+                h.rank >= size || h.token != token || served[h.rank])
                 continue;
             SendAll(peer.fd, static_cast<const char*>(data), bytes);
             served[h.rank] = true;
@@ -793,6 +821,7 @@ void RendezvousBcast(void* data, size_t bytes, int rank, int size, const char* a
     std::memcpy(hello.magic, kRdvMagic, sizeof(kRdvMagic));
     hello.rank = rank;
     hello.size = size;
+    hello.token = token;
     for (;;) {  // rank 0 may not be listening yet
         Fd s;
         s.fd = ::socket(AF_INET, SOCK_STREAM, 0);

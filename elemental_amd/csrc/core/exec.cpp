@@ -128,6 +128,31 @@ void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double
     for (int q = 0; q < nd; ++q) HOST_DTYPE_SWITCH(t, S, cpu_copy<S>(d[q], axpy, alpha));
 }
 
+void ContractSum(Device dev, DType t, Int m, Int n, void* dst, Int dcs, Int drs, const ContractSource* src,
+                 int nsrc, double alpha, hipStream_t s) {
+    if (m <= 0 || n <= 0 || nsrc <= 0) return;
+    if (dev == Device::GPU) {
+        const int cap = s != nullptr && s == Runtime::Get().CommStream() ? CommCopyWGs() : 0;
+        for (int q0 = 0; q0 < nsrc; q0 += kern::kMaxContractSources) {
+            kern::ContractSum c{};
+            c.m = m; c.n = n; c.dst = dst; c.dcs = dcs; c.drs = drs;
+            c.nsrc = std::min(nsrc - q0, kern::kMaxContractSources);
+            for (int q = 0; q < c.nsrc; ++q) {
+                c.src[q] = src[q0 + q].p;
+                c.scs[q] = src[q0 + q].cs;
+                c.srs[q] = src[q0 + q].rs;
+            }
+            check(kern::contract_sum(static_cast<int>(t), c, alpha, s, cap), "contract_sum");
+        }
+        return;
+    }
+    // host: the same per-source axpys, in order
+    for (int q = 0; q < nsrc; ++q) {
+        const Copy2D d{m, n, src[q].p, src[q].cs, src[q].rs, dst, dcs, drs};
+        HOST_DTYPE_SWITCH(t, S, cpu_copy<S>(d, true, alpha));
+    }
+}
+
 namespace {
 template <typename TS, typename TD>
 void cpu_convert(const Copy2D& d) {

@@ -14,6 +14,12 @@ namespace exec {
 using kern::Copy2D;
 
 void Copy2DBatch(Device dev, DType t, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s);
+// dst(i,j) += alpha*src_q(i,j) for every q in order, each rounded to the storage
+// type: the rank-ordered sum of AxpyContract in one pass over dst (any number of
+// sources: groups of kern::kMaxContractSources, in order)
+struct ContractSource { const void* p; Int cs, rs; };
+void ContractSum(Device dev, DType t, Int m, Int n, void* dst, Int dcs, Int drs, const ContractSource* src,
+                 int nsrc, double alpha, hipStream_t s);
 // dst(i,j) = (dst type) src(i,j): Copy_GPU_impl<SrcT,DestT> (Copy.cu:93-205)
 void Convert2D(Device dev, DType src_t, DType dst_t, const Copy2D& d, hipStream_t s);
 void Gemm(Device dev, DType t, bool ta, bool tb, Int m, Int n, Int k, double alpha,

@@ -242,19 +242,44 @@ void TransferFinish(TransferJob& j) {
             if (q != me && j.rc[q] > 0) unpack.push_back(unpack_desc(q));
         exec::Copy2DBatch(dev, t, unpack.data(), static_cast<int>(unpack.size()), false, 0.0, st);
     } else {
-        // sum contributions in rank order (deterministic); one launch per source
-        // so two sources never update the same element concurrently
-        for (int q = 0; q < p; ++q) {
+        // sum contributions in rank order (deterministic).  When every source
+        // covers the same destination pattern (the reduce-scatters of SUMMA_A /
+        // B / Dot: each source holds all of what the receiver owns) one launch
+        // reads every portion and B once (AxpyContract.hpp:475-478's single
+        // InterleaveMatrixUpdate); otherwise one axpy launch per source, so two
+        // sources never update the same element concurrently.  Both round to the
+        // storage type after each source: identical results.
+        std::vector<int> srcs;
+        for (int q = 0; q < p; ++q)
+            if (q == me ? j.in[me].count() > 0 : j.rc[q] > 0) srcs.push_back(q);
+        auto same_dst = [&](const PairPlan& a, const PairPlan& b) {
+            return a.rows.count == b.rows.count && a.cols.count == b.cols.count && a.rows.dst0 == b.rows.dst0 &&
+                   a.cols.dst0 == b.cols.dst0 && a.rows.dst_step == b.rows.dst_step &&
+                   a.cols.dst_step == b.cols.dst_step;
+        };
+        bool fused = srcs.size() > 1;
+        for (size_t i = 1; i < srcs.size() && fused; ++i) fused = same_dst(j.in[srcs[0]], j.in[srcs[i]]);
+        auto source_desc = [&](int q) {
             if (q == me) {
-                if (j.in[me].count() > 0) {
-                    const PairPlan& pl = j.in[me];
-                    kern::Copy2D d{pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
-                                   pl.cols.src_step * A.LDim(), At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
-                                   pl.cols.dst_step * B.LDim()};
-                    exec::Copy2DBatch(dev, t, &d, 1, true, j.alpha, st);
-                }
-            } else if (j.rc[q] > 0) {
-                auto d = unpack_desc(q);
+                const PairPlan& pl = j.in[me];
+                return kern::Copy2D{pl.rows.count, pl.cols.count, At(A, pl.rows.src0, pl.cols.src0), pl.rows.src_step,
+                                    pl.cols.src_step * A.LDim(), At(B, pl.rows.dst0, pl.cols.dst0), pl.rows.dst_step,
+                                    pl.cols.dst_step * B.LDim()};
+            }
+            return unpack_desc(q);
+        };
+        if (fused) {
+            std::vector<exec::ContractSource> cs;
+            for (int q : srcs) {
+                const kern::Copy2D d = source_desc(q);
+                cs.push_back({d.src, d.scs, d.srs});
+            }
+            const kern::Copy2D d0 = source_desc(srcs[0]);
+            exec::ContractSum(dev, t, d0.m, d0.n, d0.dst, d0.dcs, d0.drs, cs.data(), static_cast<int>(cs.size()),
+                              j.alpha, st);
+        } else {
+            for (int q : srcs) {
+                const kern::Copy2D d = source_desc(q);
                 exec::Copy2DBatch(dev, t, &d, 1, true, j.alpha, st);
             }
         }

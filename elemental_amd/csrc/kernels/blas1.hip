@@ -140,6 +140,60 @@ __global__ __launch_bounds__(NT) void copy2d_kernel(CopyBatch b, double alpha) {
     }
 }
 
+// Rank-ordered contraction sum (kernels.hpp ContractSum): rows over the lanes
+// of gridDim.x workgroups (N = 16 B / element per lane), columns over
+// gridDim.y.  Every source is read once and dst once each way; with unit row
+// stride and 16-B aligned columns on every operand each access is one 16-B
+// vector.  The source loop is fully unrolled so the descriptor's arrays are
+// indexed by constants (kernel arguments, never a private copy).
+template <typename T>
+__global__ __launch_bounds__(NT) void contract_sum_kernel(ContractSum c, double alpha) {
+    using E = Elem<T>;
+    using S = typename E::storage;
+    constexpr int N = V16<S>::N;
+    const auto a = (typename E::compute)alpha;
+    S* dst = static_cast<S*>(c.dst);
+    auto al16 = [](const void* p, i64 ld) {
+        return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * (i64)sizeof(S)) % 16 == 0;
+    };
+    bool vec = c.dcs == 1 && al16(dst, c.n > 1 ? c.drs : 0);
+#pragma unroll
+    for (int q = 0; q < kMaxContractSources; ++q)
+        if (q < c.nsrc) vec = vec && c.scs[q] == 1 && al16(c.src[q], c.n > 1 ? c.srs[q] : 0);
+    const i64 mv = (c.m + N - 1) / N;
+    for (i64 j = blockIdx.y; j < c.n; j += gridDim.y) {
+        for (i64 iv = (i64)blockIdx.x * NT + threadIdx.x; iv < mv; iv += (i64)gridDim.x * NT) {
+            const i64 i = iv * N;
+            S* y = dst + j * c.drs + i * c.dcs;
+            if (vec && i + N <= c.m) {
+                V16<S> x[kMaxContractSources];
+#pragma unroll
+                for (int q = 0; q < kMaxContractSources; ++q)
+                    if (q < c.nsrc) x[q] = *reinterpret_cast<const V16<S>*>(static_cast<const S*>(c.src[q]) + j * c.srs[q] + i);
+                V16<S> acc = *reinterpret_cast<const V16<S>*>(y);
+#pragma unroll
+                for (int q = 0; q < kMaxContractSources; ++q)
+                    if (q < c.nsrc) {
+#pragma unroll
+                        for (int e = 0; e < N; ++e) acc.v[e] = E::store(E::load(acc.v[e]) + a * E::load(x[q].v[e]));
+                    }
+                *reinterpret_cast<V16<S>*>(y) = acc;
+            } else {
+                for (int e = 0; e < N && i + e < c.m; ++e) {
+                    S acc = y[e * c.dcs];
+#pragma unroll
+                    for (int q = 0; q < kMaxContractSources; ++q)
+                        if (q < c.nsrc) {
+                            const S xv = static_cast<const S*>(c.src[q])[j * c.srs[q] + (i + e) * c.scs[q]];
+                            acc = E::store(E::load(acc) + a * E::load(xv));
+                        }
+                    y[e * c.dcs] = acc;
+                }
+            }
+        }
+    }
+}
+
 // Type-converting strided copy (Copy_GPU_impl<SrcT,DestT>, Copy.cu:93-205):
 // the same two shapes as copy2d_kernel (direct when both sides walk the same
 // unit-stride dimension, LDS-staged 64x64 tile otherwise); the tile holds the
@@ -682,6 +736,20 @@ hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double al
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t contract_sum(int dtype, const ContractSum& c, double alpha, hipStream_t s, int max_wgs) {
+    if (c.m <= 0 || c.n <= 0 || c.nsrc <= 0) return hipSuccess;
+    if (c.nsrc > kMaxContractSources) return hipErrorInvalidValue;
+    const int es = dtype == ELX_F64 ? 8 : dtype == ELX_F32 ? 4 : 2;
+    const i64 mv = (c.m + 16 / es - 1) / (16 / es);
+    // ~8 workgroups per CU in total, under the caller's cap
+    const i64 gy = std::min<i64>(c.n, 4096);
+    i64 gx = std::max<i64>(1, std::min<i64>((mv + NT - 1) / NT, std::max<i64>(1, 2048 / gy)));
+    if (max_wgs > 0) gx = std::max<i64>(1, std::min<i64>(gx, max_wgs / gy));
+    const dim3 grid((unsigned)gx, (unsigned)gy);
+    ELX_DTYPE_SWITCH(dtype, T, hipLaunchKernelGGL((contract_sum_kernel<T>), grid, dim3(NT), 0, s, c, alpha));
+    return hipGetLastError();
 }
 
 hipError_t convert2d(int sdt, int ddt, const Copy2D& d, hipStream_t s) {

@@ -124,6 +124,22 @@ constexpr int kMaxCopyBatch = 16;
 // max_wgs > 0 caps the workgroups of the launch (grid-stride loops cover the rest)
 hipError_t copy2d_batch(int dtype, const Copy2D* d, int nd, bool axpy, double alpha, hipStream_t s, int max_wgs = 0);
 
+// Rank-ordered reduction of a ReduceScatter's contributions (AxpyContract,
+// AxpyContract.hpp:462-478): for every (i,j) of the common destination
+// pattern, dst(i,j) += alpha*src_q(i,j) for q = 0, 1, ... in order, rounded to
+// the storage type after each source -- bit-identical to one copy2d_batch axpy
+// launch per source, but dst is read and written once ((nsrc + 2) elements of
+// traffic instead of 3 nsrc).
+constexpr int kMaxContractSources = 16;
+struct ContractSum {
+    i64 m, n;
+    void* dst; i64 dcs, drs;
+    int nsrc;
+    const void* src[kMaxContractSources];
+    i64 scs[kMaxContractSources], srs[kMaxContractSources];
+};
+hipError_t contract_sum(int dtype, const ContractSum& c, double alpha, hipStream_t s, int max_wgs = 0);
+
 // Type-converting strided copy: dst(i,j) = (dst type) src(i,j), one rounding (elem.hpp).
 hipError_t convert2d(int src_dtype, int dst_dtype, const Copy2D& d, hipStream_t s);
 hipError_t fill2d(int dtype, i64 m, i64 n, double v, void* A, i64 lda, hipStream_t s);

@@ -112,8 +112,9 @@ const BinConfig& Bins() {
     return c;
 }
 constexpr size_t kGranule = 512;  // every block is a multiple of 512 B (256-B aligned pointers)
-size_t RoundUp(size_t b, size_t g) { return (b + g - 1) / g * g; }
 constexpr size_t kSizeMax = std::numeric_limits<size_t>::max();
+// round b up to a multiple of g; 0 (no bin) when that does not fit in size_t
+size_t RoundUp(size_t b, size_t g) { return b > kSizeMax - (g - 1) ? 0 : (b + g - 1) / g * g; }
 size_t MulSat(size_t a, unsigned g) { return a > kSizeMax / g ? kSizeMax : a * g; }
 // growth^k, saturating at SIZE_MAX
 size_t PowSat(unsigned g, unsigned k) {
@@ -126,6 +127,8 @@ const char* StreamTag(hipStream_t s, hipStream_t compute, hipStream_t comm) {
 }
 }  // namespace
 
+// 0 when no bin can hold b (the rounding would overflow size_t); Alloc then
+// reports out-of-memory instead of handing out a zero-byte block
 size_t Runtime::BinBytes(size_t b, bool* cacheable) {
     const BinConfig& c = Bins();
     if (cacheable) *cacheable = true;
@@ -140,6 +143,7 @@ size_t Runtime::BinBytes(size_t b, bool* cacheable) {
         }
         size_t p = PowSat(c.growth, c.min_bin);
         while (p < b && p != kSizeMax) p = MulSat(p, c.growth);
+        if (p < b) return 0;  // saturated below the request: no bin
         return RoundUp(std::max<size_t>(p, 1), kGranule);
     }
     // powers of two up to 1 MiB (CUB bin_growth 2), then eight bins per octave
@@ -151,8 +155,7 @@ size_t Runtime::BinBytes(size_t b, bool* cacheable) {
     }
     size_t top = size_t(1) << 20;
     while ((top << 1) <= b && top < (size_t(1) << 62)) top <<= 1;
-    const size_t step = top / 8;
-    return (b + step - 1) / step * step;
+    return RoundUp(b, top / 8);
 }
 
 hipEvent_t Runtime::EventLocked() {
@@ -162,12 +165,17 @@ hipEvent_t Runtime::EventLocked() {
     return ev;
 }
 
-void* Runtime::Backing(size_t bin, hipStream_t) {
+void* Runtime::Backing(size_t bin) {
+    // called without mu_: hipMalloc never runs under the allocator's lock
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, bin);
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
         (void)hipGetLastError();
-        ReleaseCachedLocked(0);  // give the cache back and retry once
+        {  // give the cache back and retry once, after every release has landed
+            std::lock_guard<std::mutex> lk(mu_);
+            ReleaseCachedLocked(0);
+        }
+        WaitReleases();
         e = hipMalloc(&p, bin);
     }
     if (e != hipSuccess) {
@@ -175,34 +183,81 @@ void* Runtime::Backing(size_t bin, hipStream_t) {
         size_t fr = 0, tot = 0;
         (void)hipMemGetInfo(&fr, &tot);
         throw HIPError(Cat("elx_pool_alloc: ", hipGetErrorString(e), " (", bin, " bytes requested, ",
-                           fr, " bytes available, ", tot, " bytes total, ", cached_, " cached)"));
+                           fr, " bytes available, ", tot, " bytes total)"));
     }
-    backing_ += bin;
     return p;
 }
 
-void Runtime::ReturnLocked(void* p, size_t bin, hipEvent_t ready) {
-    // The block's last use is complete before the driver sees it again: the
-    // host waits for the free's event (hipFree synchronizes as well), as CUB's
-    // DeviceFree returns over-cap blocks with a synchronous cudaFree.
-    ELX_CHECK_HIP(hipEventSynchronize(ready));
-    ELX_CHECK_HIP(hipFree(p));
-    backing_ -= bin;
-    spare_events_.push_back(ready);
+void Runtime::QueueReleaseLocked(void* p, size_t bin, hipEvent_t ready) {
+    // The block goes back to the driver once its free's event completed (CUB
+    // returns over-cap blocks with a synchronous cudaFree), but neither the
+    // event wait nor hipFree (which waits for the whole device) run on the
+    // caller's thread or under mu_: the release thread does both.
+    pending_.push_back(Pending{p, bin, ready});
+    if (!releaser_started_) {
+        releaser_started_ = true;
+        releaser_ = std::thread([this] { ReleaseLoop(); });
+        // drain before the HIP runtime tears down (registered after hipInit, so
+        // it runs before the runtime's own exit handlers)
+        std::atexit([] { Runtime::Get().StopReleaser(); });
+    }
+    release_cv_.notify_one();
     if (Bins().debug)
-        std::fprintf(stderr, "elx_pool[dev %d]: returned block %p (%zu bytes) to the driver (cached %zu, live %zu)\n",
-                     device_, p, bin, cached_, live_bin_);
+        std::fprintf(stderr, "elx_pool[dev %d]: queued block %p (%zu bytes) for release to the driver "
+                             "after event %p (cached %zu, live %zu)\n",
+                     device_, p, bin, (void*)ready, cached_, live_bin_);
+}
+
+void Runtime::ReleaseLoop() {
+    (void)hipSetDevice(device_);
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+        release_cv_.wait(lk, [this] { return !pending_.empty() || stop_; });
+        if (pending_.empty()) break;  // stop_ with nothing left
+        const Pending x = pending_.front();
+        pending_.pop_front();
+        releasing_ = true;
+        lk.unlock();
+        const hipError_t e1 = hipEventSynchronize(x.ready);
+        const hipError_t e2 = hipFree(x.p);
+        if (e1 != hipSuccess || e2 != hipSuccess)
+            std::fprintf(stderr, "elx_pool[dev %d]: releasing block %p failed: %s / %s\n", device_, x.p,
+                         hipGetErrorString(e1), hipGetErrorString(e2));
+        lk.lock();
+        releasing_ = false;
+        backing_ -= x.bin;
+        spare_events_.push_back(x.ready);
+        if (Bins().debug)
+            std::fprintf(stderr, "elx_pool[dev %d]: returned block %p (%zu bytes) to the driver (cached %zu, live %zu)\n",
+                         device_, x.p, x.bin, cached_, live_bin_);
+        idle_cv_.notify_all();
+    }
+}
+
+void Runtime::WaitReleases() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_cv_.wait(lk, [this] { return pending_.empty() && !releasing_; });
+}
+
+void Runtime::StopReleaser() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!releaser_started_ || stop_) return;
+        stop_ = true;
+    }
+    release_cv_.notify_one();
+    if (releaser_.joinable()) releaser_.join();
 }
 
 void Runtime::ReleaseCachedLocked(size_t keep) {
-    // largest blocks first, each back to the driver once its free's event is done
+    // largest blocks first, each queued for release behind its free's event
     while (cached_ > keep && !cache_.empty()) {
         auto it = std::prev(cache_.end());
         const size_t bin = it->first;
         const Cached c = it->second;
         cached_ -= bin;
         cache_.erase(it);
-        ReturnLocked(c.p, bin, c.ready);
+        QueueReleaseLocked(c.p, bin, c.ready);
     }
 }
 
@@ -212,48 +267,59 @@ void* Runtime::Alloc(size_t bytes, hipStream_t s) {
     if (!s) s = compute_;
     bool cacheable = true;
     const size_t bin = BinBytes(bytes, &cacheable);
-    std::lock_guard<std::mutex> lk(mu_);
-    void* p = nullptr;
+    if (bin < bytes)  // BinBytes' overflow marker (0): no bin holds the request
+        throw HIPError(Cat("elx_pool_alloc: out of memory (", bytes, " bytes requested: larger than any block)"));
     // ELX_POOL_CACHE=0 (debug): no caching, every request from the backing pool
     static const bool nocache = [] { const char* e = std::getenv("ELX_POOL_CACHE"); return e && e[0] == '0'; }();
-    auto [lo, hi] = cache_.equal_range(bin);
-    if (nocache || !cacheable) lo = hi;
-    if (lo != hi) {
-        // prefer a block last used on this stream, then one whose free has
-        // completed, then any (ordered behind its free's event)
-        auto pick = hi;
-        for (auto it = lo; it != hi; ++it)
-            if (it->second.stream == s) { pick = it; break; }
-        if (pick == hi)
+    void* p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto [lo, hi] = cache_.equal_range(bin);
+        if (nocache || !cacheable) lo = hi;
+        if (lo != hi) {
+            // prefer a block last used on this stream, then one whose free has
+            // completed, then any (ordered behind its free's event)
+            auto pick = hi;
             for (auto it = lo; it != hi; ++it)
-                if (hipEventQuery(it->second.ready) == hipSuccess) { pick = it; break; }
-        if (pick == hi) pick = lo;
-        const bool cross = pick->second.stream != s;
-        const bool waits = hipEventQuery(pick->second.ready) != hipSuccess;
-        if (waits) ELX_CHECK_HIP(hipStreamWaitEvent(s, pick->second.ready, 0));
-        p = pick->second.p;
-        if (Bins().debug)
-            std::fprintf(stderr,
-                         "elx_pool[dev %d]: reused cached block %p (%zu bytes, bin %zu) for stream %p%s "
-                         "(freed on stream %p%s, event %p%s)\n",
-                         device_, p, bytes, bin, (void*)s, StreamTag(s, compute_, comm_), (void*)pick->second.stream,
-                         StreamTag(pick->second.stream, compute_, comm_), (void*)pick->second.ready,
-                         cross ? (waits ? ": cross-stream reuse, the new stream waits on the event"
-                                        : ": cross-stream reuse, event already complete")
-                               : ": same stream");
-        spare_events_.push_back(pick->second.ready);
-        cached_ -= bin;
-        cache_.erase(pick);
-    } else {
-        p = Backing(bin, s);
+                if (it->second.stream == s) { pick = it; break; }
+            if (pick == hi)
+                for (auto it = lo; it != hi; ++it)
+                    if (hipEventQuery(it->second.ready) == hipSuccess) { pick = it; break; }
+            if (pick == hi) pick = lo;
+            const bool cross = pick->second.stream != s;
+            const bool waits = hipEventQuery(pick->second.ready) != hipSuccess;
+            if (waits) ELX_CHECK_HIP(hipStreamWaitEvent(s, pick->second.ready, 0));
+            p = pick->second.p;
+            if (Bins().debug)
+                std::fprintf(stderr,
+                             "elx_pool[dev %d]: reused cached block %p (%zu bytes, bin %zu) for stream %p%s "
+                             "(freed on stream %p%s, event %p%s)\n",
+                             device_, p, bytes, bin, (void*)s, StreamTag(s, compute_, comm_),
+                             (void*)pick->second.stream, StreamTag(pick->second.stream, compute_, comm_),
+                             (void*)pick->second.ready,
+                             cross ? (waits ? ": cross-stream reuse, the new stream waits on the event"
+                                            : ": cross-stream reuse, event already complete")
+                                   : ": same stream");
+            spare_events_.push_back(pick->second.ready);
+            cached_ -= bin;
+            cache_.erase(pick);
+            live_[p] = Live{bytes, bin, cacheable};
+            in_use_ += bytes;
+            live_bin_ += bin;
+        }
+    }
+    if (!p) {
+        p = Backing(bin);
+        std::lock_guard<std::mutex> lk(mu_);
+        backing_ += bin;
+        live_[p] = Live{bytes, bin, cacheable};
+        in_use_ += bytes;
+        live_bin_ += bin;
         if (Bins().debug)
             std::fprintf(stderr, "elx_pool[dev %d]: allocated new block %p (%zu bytes, bin %zu%s) for stream %p%s\n",
                          device_, p, bytes, bin, cacheable ? "" : ", uncached", (void*)s,
                          StreamTag(s, compute_, comm_));
     }
-    live_[p] = Live{bytes, bin, cacheable};
-    in_use_ += bytes;
-    live_bin_ += bin;
     // ELX_POOL_POISON=1 (debug): every block handed out is filled with 0xFF
     // bytes (NaN in every float type), so a read before the first write shows up
     static const bool poison = [] { const char* e = std::getenv("ELX_POOL_POISON"); return e && e[0] == '1'; }();
@@ -275,7 +341,7 @@ void Runtime::Free(void* p, hipStream_t s) {
     live_bin_ -= l.bin;
     live_.erase(it);
     if (nocache || !l.cacheable || cached_ + l.bin > max_cached_) {
-        ReturnLocked(p, l.bin, ev);  // over the cap / uncacheable: back to the driver
+        QueueReleaseLocked(p, l.bin, ev);  // over the cap / uncacheable: back to the driver
     } else {
         cache_.emplace(l.bin, Cached{p, s, ev});
         cached_ += l.bin;
@@ -289,8 +355,11 @@ void Runtime::Free(void* p, hipStream_t s) {
 void Runtime::Trim(size_t keep) {
     EnsureGPU();
     ELX_CHECK_HIP(hipDeviceSynchronize());
-    std::lock_guard<std::mutex> lk(mu_);
-    ReleaseCachedLocked(keep);
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        ReleaseCachedLocked(keep);
+    }
+    WaitReleases();
 }
 
 void Runtime::SetMaxCached(size_t bytes) {
@@ -312,6 +381,7 @@ void Runtime::Stats(size_t& reserved, size_t& in_use) {
 }
 
 size_t Runtime::BackingReserved() {
+    WaitReleases();
     std::lock_guard<std::mutex> lk(mu_);
     return backing_;
 }

@@ -20,15 +20,21 @@
 //  * cached bytes are capped by H_CUB_MAX_CACHED_SIZE / ELX_POOL_MAX_CACHED /
 //    elx_pool_set_max_cached (default: unbounded, as CUB's INVALID_SIZE); a
 //    block that does not fit under the cap, an uncacheable block and, with
-//    ELX_POOL_CACHE=0, every block leaves the allocator: the host waits for its
-//    free's event and hipFrees it, so the memory returns to the driver (CUB's
-//    synchronous cudaFree);
+//    ELX_POOL_CACHE=0, every block leaves the allocator: it is queued for the
+//    allocator's release thread, which waits for the free's event and hipFrees
+//    it, so the memory returns to the driver as under CUB's synchronous
+//    cudaFree, but the freeing thread returns at once and no event wait or
+//    hipFree ever runs under the allocator's lock (a free never stalls the host
+//    or another thread's Alloc / Free); Trim, elx_pool_backing_reserved and an
+//    out-of-memory retry wait for the queued releases;
+//  * a request no bin can hold (its rounding overflows) fails with
+//    out-of-memory;
 //  * the backing store is hipMalloc / hipFree, as under hipCUB's
 //    CachingDeviceAllocator (cudaMalloc / cudaFree); a block goes back to the
 //    driver only once the host has seen its free's event complete.  Not the
 //    driver's stream-ordered pool (hipMallocFromPoolAsync): round 5 measured it
 //    on this ROCm (tools/pool_race_probe.hip, tools/pool_trim_probe.hip,
-//    profiles/r05_pool_probes.log): a hipFreeAsync'd block whose earlier work
+//    profiles/r05_pool_race_probe.log, profiles/r05_pool_trim_probe.log): a hipFreeAsync'd block whose earlier work
 //    is still queued is re-backed or handed out before that work runs; with
 //    follow-event-dependencies on, a stream that once waited on an OLDER event
 //    of the freeing stream receives the block at once; and even with every
@@ -43,8 +49,11 @@
 //    return and release to stderr.
 #pragma once
 #include "../common.hpp"
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -72,8 +81,9 @@ public:
     void Trim(size_t keep);
     // reserved = live + cached bin bytes; in_use = requested bytes still live
     void Stats(size_t& reserved, size_t& in_use);
-    // bytes held from the driver (hipMalloc'd, not yet hipFree'd): live +
-    // cached blocks; 0 before the first GPU use
+    // bytes held from the driver (hipMalloc'd, not yet hipFree'd) once the
+    // queued releases have landed (waits for them): live + cached blocks; 0
+    // before the first GPU use
     size_t BackingReserved();
     void SetMaxCached(size_t bytes);
     size_t MaxCached();
@@ -84,13 +94,23 @@ public:
 private:
     struct Cached { void* p; hipStream_t stream; hipEvent_t ready; };
     struct Live { size_t requested, bin; bool cacheable; };
+    struct Pending { void* p; size_t bin; hipEvent_t ready; };
     Runtime() = default;
-    void* Backing(size_t bin, hipStream_t s);
+    // hipMalloc a new block (without mu_; on out-of-memory: release the cache,
+    // wait for the releases, retry once)
+    void* Backing(size_t bin);
     void ReleaseCachedLocked(size_t keep);
-    // give a block back to the driver once the host saw `ready` complete
-    void ReturnLocked(void* p, size_t bin, hipEvent_t ready);
+    // hand a block to the release thread: hipFree'd once `ready` completed
+    void QueueReleaseLocked(void* p, size_t bin, hipEvent_t ready);
+    void ReleaseLoop();
+    void WaitReleases();  // until every queued release landed (takes mu_)
+    void StopReleaser();  // at exit: drain the queue, join the thread
     hipEvent_t EventLocked();
     std::mutex mu_;
+    std::condition_variable release_cv_, idle_cv_;
+    std::deque<Pending> pending_;
+    std::thread releaser_;
+    bool releaser_started_ = false, releasing_ = false, stop_ = false;
     bool gpu_ready_ = false;
     int device_ = -1;
     int reserved_cus_ = 0;

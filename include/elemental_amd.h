@@ -143,7 +143,8 @@ int elx_pool_set_max_cached(size_t bytes);
 int elx_pool_max_cached(size_t* bytes);
 /* the bin a request of `bytes` is served from (reserved bytes per block);
  * H_CUB_BIN_GROWTH / H_CUB_MIN_BIN / H_CUB_MAX_BIN select CUB's geometric bins
- * (cub.cpp:21-35, read once per process) */
+ * (cub.cpp:21-35, read once per process); 0 when no bin can hold the request
+ * (its rounding overflows size_t: elx_pool_alloc fails with out-of-memory) */
 size_t elx_pool_bin_bytes(size_t bytes);
 /* 1 when a request of `bytes` is cached on free, 0 when it is above
  * H_CUB_MAX_BIN's bin (an own-size block returned to the driver on free) */

@@ -462,9 +462,14 @@ def blas1_worker(rank: int, world: int, port: int, height: int, device: int, see
         E = el.DistMatrix(g, el.F64, el.MC, el.MR, device, height=m, width=n)
         E.set_local(oracle.local_block(Yg, el.MC, el.MR, r, c, g.vc_rank))
         el.AxpyContract(1.0, D, E)
-        tot = sum(range(1, c + 1))
-        want = oracle.local_block(Yg + tot * Xg, el.MC, el.MR, r, c, g.vc_rank)
-        assert np.allclose(E.get_local(), want, rtol=0, atol=1e-13), "AxpyContract"
+        # bit-exact: the c contributions summed in rank order (AxpyContract.hpp:
+        # 462-478), each addition rounded -- one fused pass over E on the GPU,
+        # one axpy per source on the host, the same arithmetic
+        want = Yg.copy()
+        for q in range(c):
+            want = want + Xg * (q + 1)
+        want = oracle.local_block(want, el.MC, el.MR, r, c, g.vc_rank)
+        assert np.array_equal(E.get_local(), want), "AxpyContract"
         # EntrywiseMap into another distribution
         F = el.DistMatrix(g, el.F64, el.STAR, el.VR, device)
         el.EntrywiseMap(el.L.MAP_SQUARE if hasattr(el, "L") else 3, Xm, F)
@@ -515,6 +520,19 @@ def blas1_worker(rank: int, world: int, port: int, height: int, device: int, see
             sq = stored(xf.astype(np.float32) * xf.astype(np.float32))
             assert np.array_equal(_bits(Xd.get_local()), _bits(oracle.local_block(sq, el.MC, el.MR, r, c,
                                                                                   g.vc_rank))), f"X.*X in place {fmt}"
+            # 16-bit AxpyContract over MR: rank-ordered, each sum in f32 rounded
+            # to the storage format before the next source
+            contrib = [stored(xf.astype(np.float32) * np.float32(q + 1)) for q in range(c)]
+            Dd = el.DistMatrix(g, dt, el.MC, el.STAR, device, height=m, width=n)
+            Dd.set_local(oracle.local_block(contrib[g.mr_rank], el.MC, el.STAR, r, c, g.vc_rank))
+            Ed = el.DistMatrix(g, dt, el.MC, el.MR, device, height=m, width=n)
+            Ed.set_local(oracle.local_block(Y16, el.MC, el.MR, r, c, g.vc_rank))
+            el.AxpyContract(1.0, Dd, Ed)
+            acc = Y16
+            for q in range(c):
+                acc = stored(oracle.to_f64(acc, fmt).astype(np.float32) + oracle.to_f64(contrib[q], fmt).astype(np.float32))
+            assert np.array_equal(_bits(Ed.get_local()), _bits(oracle.local_block(acc, el.MC, el.MR, r, c,
+                                                                                  g.vc_rank))), f"AxpyContract {fmt}"
         finish()
     except Exception:
         traceback.print_exc()

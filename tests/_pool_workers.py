@@ -136,8 +136,53 @@ def debug_trace_cross_stream():
     el.device_synchronize()
 
 
+def release_off_the_lock():
+    """Run with H_CUB_MAX_CACHED_SIZE=0, so every free is over the cap and its
+    block goes back to the driver.  A block freed behind a ~0.2 s spin returns
+    to the host at once (the event wait and hipFree happen on the allocator's
+    release thread, never under its lock), a second thread's Alloc / Free
+    completes while the spin still runs, and once the device is idle the
+    bytes are back with the driver."""
+    import threading
+    import time
+    s1, s2 = _stream(), _stream()
+    base = el.pool_backing_reserved()
+    n = (64 << 20) // 8
+    X = ctypes.c_void_p()
+    L.call("elx_pool_alloc", ctypes.byref(X), n * 8, s1)
+    L.call("elx_fill2d", L.F64, n, 1, 1.0, X, n, s1)
+    L.call("elx_stream_synchronize", s1)
+    _spin(s1)
+    spun = torch.cuda.Event()
+    with torch.cuda.stream(torch.cuda.ExternalStream(s1.value)):
+        spun.record()
+    t0 = time.perf_counter()
+    L.call("elx_pool_free", X, s1)
+    dt_free = time.perf_counter() - t0
+    other = {}
+
+    def second_thread():
+        t = time.perf_counter()
+        q = ctypes.c_void_p()
+        L.call("elx_pool_alloc", ctypes.byref(q), 32 << 20, s2)
+        L.call("elx_pool_free", q, s2)
+        other["dt"] = time.perf_counter() - t
+
+    th = threading.Thread(target=second_thread)
+    th.start()
+    th.join(timeout=10)
+    spin_running = not spun.query()
+    el.device_synchronize()
+    back = el.pool_backing_reserved()
+    print(f"free {dt_free * 1e3:.3f} ms, second thread alloc+free {other.get('dt', -1) * 1e3:.3f} ms, "
+          f"spin still running after it: {spin_running}, backing {base} -> {back}", flush=True)
+    assert dt_free < 0.010, dt_free
+    assert "dt" in other and spin_running, (other, spin_running)
+    assert back == base, (base, back)
+
+
 CASES = {f.__name__: f for f in (pool_free_after_delayed_reader, view_on_other_stream, set_stream_owned,
-                                  debug_trace_cross_stream)}
+                                  debug_trace_cross_stream, release_off_the_lock)}
 
 if __name__ == "__main__":
     for name in sys.argv[1:]:

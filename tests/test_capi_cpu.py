@@ -86,6 +86,14 @@ def test_pool_bins_and_cap_setting_without_device():
         assert b <= bb <= b * 1.125 and bb % (128 << 10) == 0 and bb > prev
         assert lib.elx_pool_bin_cacheable(b) == 1
         prev = bb
+    # requests whose rounding would overflow size_t get no bin (0): Alloc reports
+    # out-of-memory instead of handing out a zero-byte block (e.g. El.hpp's
+    # SendRecv scratch for a negative int count cast to size_t)
+    smax = (1 << 64) - 1
+    for b in (smax, smax - 5, (1 << 64) - (1 << 58)):
+        assert lib.elx_pool_bin_bytes(b) == 0, b
+    assert lib.elx_pool_bin_bytes(1 << 62) == 1 << 62
+    assert lib.elx_pool_bin_bytes((1 << 63) + 1) == (1 << 63) + (1 << 59)
     old = L.ctypes.c_size_t()
     L.call("elx_pool_max_cached", L.ctypes.byref(old))
     try:
@@ -130,7 +138,8 @@ def test_pool_cub_bin_knobs(env):
     import os
     import subprocess
     import sys
-    sizes = [0, 1, 100, 511, 512, 513, 4096, 5000, 65537, 1 << 20, (1 << 20) + 1, 3 << 20, 123456789, 5 << 30]
+    sizes = [0, 1, 100, 511, 512, 513, 4096, 5000, 65537, 1 << 20, (1 << 20) + 1, 3 << 20, 123456789, 5 << 30,
+             (1 << 64) - 1]
     code = ("import json,sys; sys.path.insert(0, %r); from elemental_amd import _lib as L; lib = L.lib(); "
             "print(json.dumps([[lib.elx_pool_bin_bytes(b), lib.elx_pool_bin_cacheable(b)] for b in %r]))"
             % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), sizes))
@@ -143,6 +152,9 @@ def test_pool_cub_bin_knobs(env):
     mn = int(env.get("H_CUB_MIN_BIN", 1))
     mx = int(env["H_CUB_MAX_BIN"]) if "H_CUB_MAX_BIN" in env else None
     want = [list(_cub_bin(b, g, mn, mx)) for b in sizes]
+    # SIZE_MAX: no growth^k holds it, and an own-size block would overflow the
+    # 512-B rounding: no bin (0), whichever way it is classified
+    want[-1][0] = 0
     assert got == want, list(zip(sizes, got, want))
 
 

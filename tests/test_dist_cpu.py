@@ -172,7 +172,7 @@ def test_uniform_reference_draws(world, height):
     _spawn(W.uniform_worker, world, height, el.CPU)
 
 
-@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2), (8, 2)])
 def test_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.CPU, 5)
 

@@ -100,8 +100,9 @@ def test_rendezvous_ignores_stray_connections():
             assert time.monotonic() < deadline
             time.sleep(0.05)
     import struct
-    for payload in (b"GET / HTTP/1.0\r\n\r\n", b"ELXRDV01" + struct.pack("<ii", 1, 7),
-                    b"ELXRDV01" + struct.pack("<ii", 0, 3), b"ELXRDV01" + struct.pack("<ii", 5, 3)):
+    for payload in (b"GET / HTTP/1.0\r\n\r\n", b"ELXRDV02" + struct.pack("<iiQ", 1, 7, 0),
+                    b"ELXRDV02" + struct.pack("<iiQ", 0, 3, 0), b"ELXRDV02" + struct.pack("<iiQ", 5, 3, 0),
+                    b"ELXRDV01" + struct.pack("<ii", 1, 3)):
         c = so.create_connection(("127.0.0.1", port), timeout=2)
         c.sendall(payload)
         strays.append(c)
@@ -113,6 +114,54 @@ def test_rendezvous_ignores_stray_connections():
         c.settimeout(2)
         try:
             assert c.recv(16) == b""  # closed without the payload
+        except (so.timeout, ConnectionResetError):
+            pass
+        c.close()
+
+
+def _fnv1a64(s: str) -> int:
+    h = 14695981039346656037
+    for b in s.encode():
+        h = ((h ^ b) * 1099511628211) % (1 << 64)
+    return h
+
+
+def test_rendezvous_secret_and_loopback_bind():
+    """ELX_RENDEZVOUS_SECRET: a well-formed hello for a real rank that carries
+    another job's token (here: none) is refused and never takes that rank's
+    slot; the peers holding the secret are served.  With MASTER_ADDR 127.0.0.1,
+    rank 0 listens on the loopback address only, not on every interface."""
+    import socket as so
+    import struct
+    import psutil
+    port = _port()
+    env = dict(os.environ, ELX_RENDEZVOUS_SECRET="job-4711")
+    root = subprocess.Popen([sys.executable, WORKER, "rendezvous", "0", "3", str(port)], env=env,
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    deadline = time.monotonic() + 30
+    listen = []
+    while not listen:
+        assert time.monotonic() < deadline
+        try:
+            listen = [c for c in psutil.Process(root.pid).net_connections(kind="tcp")
+                      if c.status == psutil.CONN_LISTEN and c.laddr.port == port]
+        except psutil.NoSuchProcess:
+            break
+        time.sleep(0.05)
+    assert [c.laddr.ip for c in listen] == ["127.0.0.1"], listen
+    wrong = []
+    for tok in (0, _fnv1a64("job-4712")):
+        c = so.create_connection(("127.0.0.1", port), timeout=2)
+        c.sendall(b"ELXRDV02" + struct.pack("<iiQ", 1, 3, tok))
+        wrong.append(c)
+    peers = [subprocess.Popen([sys.executable, WORKER, "rendezvous", str(r), "3", str(port)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (1, 2)]
+    outs = [p.communicate(timeout=60) for p in [root] + peers]
+    assert all(p.returncode == 0 for p in [root] + peers), [o[1] for o in outs]
+    for c in wrong:
+        c.settimeout(2)
+        try:
+            assert c.recv(16) == b""
         except (so.timeout, ConnectionResetError):
             pass
         c.close()

@@ -69,7 +69,7 @@ def test_gpu_summa_f32():
     _spawn(W.gemm_worker, 2, 1, el.GPU, el.F32, [(65, 33, 97)], [el.GEMM_SUMMA_C, el.GEMM_SUMMA_DOT], 8, 9)
 
 
-@pytest.mark.parametrize("world,height", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("world,height", [(2, 1), (4, 2), (8, 2)])
 def test_gpu_blas1_distributed(world, height):
     _spawn(W.blas1_worker, world, height, el.GPU, 17)
 
@@ -353,9 +353,33 @@ def test_gpu_bench_stage_hang(hang, line):
     if not line:
         assert not lines
     else:
-        assert len(lines) == 1
+        assert len(lines) == 1 and p.stdout.strip() == lines[0], p.stdout  # stdout holds the line only
         rec = json.loads(lines[0])
         assert rec["value"] > 0 and rec["verify"]["ok"] and "error" in rec[hang] and "incomplete" in rec
+
+
+def test_gpu_bench_launches_its_own_ranks():
+    """`python3 bench.py --gpus 2` with no launcher (WORLD_SIZE unset): the script
+    starts its two rank processes itself (bench.launch_ranks) and the caller reads
+    exactly one line on stdout, the complete N = 2 line (host-staged panels, both
+    ranks on this box's one GPU: ELX_BENCH_COMM=host), with the residual checked
+    on its own grid and exit status 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ELX_BENCH_COMM"] = "host"
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--size", "2048", "--steps", "1",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr[-4000:]
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["grid"] == "1x2" and rec["value"] > 0
+    assert rec["residual"]["ok"] and rec["verify"]["ok"]
+    assert "collectives" in rec and "c4" not in rec and "c5" not in rec  # N > 1 default: C3 + residual only
 
 
 def _need_gpus(world):

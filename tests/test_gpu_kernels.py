@@ -155,14 +155,22 @@ def test_local_gemm_f64_one_workgroup_per_cu_exact(ta, tb, shape):
     assert np.array_equal(host(dC, (m, n), np.float64), 2.0 * (opA @ opB) - C)
 
 
+_F64_RING_CASES = [(r, sh, b) for r in ("1", "0") for sh, b in [
+    ((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0), ((2048, 4096, 2072), -1.0), ((4096, 2048, 32), 0.5)]] + [
+    ("2", (1536, 2048, 640), -1.0), ("2", (1000, 1016, 1056), 0.0), ("2", (1536, 2048, 2072), -1.0),
+    ("2", (1024, 512, 16), 0.5), ("2", (512, 512, 2048), -1.0), ("2", (520, 600, 3000), 0.0)]
+
+
+def _with_stages(cases):
+    """Each ring case in both DMA forms; the slab kernels (ring "0") only in the
+    buffer-descriptor form: they read their *_STAGE knob once per process, so a
+    per-test setting could never reach them."""
+    return [(r, sh, b, st) for r, sh, b in cases for st in ("buf", "global") if not (r == "0" and st == "global")]
+
+
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-@pytest.mark.parametrize("ring,shape,beta", [
-    (r, sh, b) for r in ("1", "0") for sh, b in [((4096, 4096, 640), -1.0), ((4000, 4040, 1056), 0.0),
-                                                 ((2048, 4096, 2072), -1.0), ((4096, 2048, 32), 0.5)]] + [
-    ("2", (1536, 2048, 640), -1.0), ("2", (1000, 1016, 1056), 0.0), ("2", (1536, 2048, 2072), -1.0),
-    ("2", (1024, 512, 16), 0.5), ("2", (512, 512, 2048), -1.0), ("2", (520, 600, 3000), 0.0)])
-@pytest.mark.parametrize("stage", ["buf", "global"])
+@pytest.mark.parametrize("ring,shape,beta,stage", _with_stages(_F64_RING_CASES))
 def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, stage, monkeypatch):
     """The fp64 ring kernel (gemm_f64r_kernel: four waves, a 5-slot LDS ring of
     32-deep K-tiles; ELX_F64G_RING=1) on 128-tile grids: many wraps of the ring
@@ -177,8 +185,6 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, stage, monkeypatch
     (partials through splitk_reduce)."""
     monkeypatch.setenv("ELX_F64G_RING", ring)
     if stage == "global":  # the 64-bit-address DMA form (operands too long for 31-bit offsets)
-        if ring == "0":
-            pytest.skip("the slab kernels read ELX_F64G_STAGE once per process")
         monkeypatch.setenv("ELX_F64G_STAGE", "g")
     m, n, k = shape
     rng = np.random.default_rng(m + k)
@@ -202,15 +208,14 @@ def test_local_gemm_f64_ring_exact(ta, tb, shape, beta, ring, stage, monkeypatch
 
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
-@pytest.mark.parametrize("ring,shape,beta", [
+@pytest.mark.parametrize("ring,shape,beta,stage", _with_stages([
     ("1", (2048, 2048, 640), -1.0), ("1", (4000, 4040, 1088), 0.0), ("1", (2048, 4096, 2072), -1.0),
     ("1", (4096, 2048, 64), 0.5),
     ("2", (1024, 1024, 2048), -1.0), ("2", (1000, 1016, 1152), 0.0), ("2", (1536, 2048, 2100), -1.0),
     ("2", (1024, 512, 128), 0.5),
     ("4", (1536, 2048, 640), -1.0), ("4", (1000, 1016, 1056), 0.0), ("4", (1536, 2048, 2100), -1.0),
     ("4", (1024, 512, 32), 0.5), ("4", (512, 512, 4096), -1.0), ("4", (520, 600, 3000), 0.0),
-    ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)])
-@pytest.mark.parametrize("stage", ["buf", "global"])
+    ("0", (4000, 4040, 1088), 0.0), ("0", (1000, 1016, 1152), 0.0)]))
 def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, stage, monkeypatch):
     """The fp32 ring kernel (gemm_f32r_kernel; ELX_F32G_RING bit 0: 128 x 128
     tiles with 64-deep K-tiles on grids of 128-tiles, bit 1: 64 x 64 tiles with
@@ -224,8 +229,6 @@ def test_local_gemm_f32_ring_exact(ta, tb, ring, shape, beta, stage, monkeypatch
     "0": the slab kernels on the ragged cases.  Integer operands: exact."""
     monkeypatch.setenv("ELX_F32G_RING", ring)
     if stage == "global":  # the 64-bit-address DMA form (operands too long for 31-bit offsets)
-        if ring == "0":
-            pytest.skip("the slab kernels read ELX_F32G_STAGE once per process")
         monkeypatch.setenv("ELX_F32G_STAGE", "g")
     m, n, k = shape
     rng = np.random.default_rng(m + k + 1)
@@ -741,6 +744,16 @@ def test_pool_delayed_reader_regression(cache):
     for c in cases:
         r = _pool_worker(c, ELX_POOL_CACHE=cache)
         assert r.returncode == 0 and f"OK {c}" in r.stdout, (c, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_pool_release_path_off_the_host():
+    """The over-cap release path (H_CUB_MAX_CACHED_SIZE=0, cub.cpp:37-43): a
+    free behind a 0.2 s spin returns to the host in < 10 ms, a second thread's
+    Alloc completes while the spin runs, and the memory is back with the driver
+    once the device is idle (runtime.hpp's contract)."""
+    r = _pool_worker("release_off_the_lock", H_CUB_MAX_CACHED_SIZE="0")
+    assert r.returncode == 0 and "OK release_off_the_lock" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    print(r.stdout.strip().splitlines()[0])
 
 
 def test_pool_debug_trace_lists_cross_stream_reuse():
