@@ -613,11 +613,16 @@ bool t64_tiles(i64 m, i64 n, i64 k) {
 //  * 64 x 64 ring on grids of at most 256 64-tiles (one round of workgroups):
 //    1024^2 x 2048 NN / TN / NT / TT 95 / 100 / 94 / 95 -> 123 / 124 / 123 / 122
 //    TF; with more (1536 x 2048^2, three per CU in turn) 128 -> 120-126: slab;
-//  * 128 x 128 ring where A is k-contiguous (TN, TT): 16384^3 TN 150.0 -> 151,
-//    TT 148.5 -> 149.5, 8192^2 x 65536 (C4's shape) 149.4 -> 151.6, 4096^3 TT
-//    145.3 -> 146.2; with A rows-contiguous (NN, NT) the slab kernel's two
-//    workgroups per CU stay ahead below 16384^3 (C3-f32's 65536 x 8192^2 panel
-//    150.1 vs 147.6, 8192^3 149.8 vs 147.4, 4096^3 NN 146.9 vs 145.4).
+//  * 128 x 128 ring, one workgroup per CU, on grids of fewer than 512
+//    128-tiles, every orientation: round 5 first measured it where A is
+//    k-contiguous (16384^3 TN 150.0 -> 151, TT 148.5 -> 149.5, 8192^2 x 65536
+//    149.4 -> 151.6); the grids where A rows-contiguous (NN, NT) then favoured
+//    the slab kernel's two workgroups per CU (8192^3, 4096^3, C3-f32's panel)
+//    are >= 512-tile grids, which now take the two-per-CU ring below.  Round 6
+//    A/B on 257..511-tile grids (profiles/r06b_f32_ring_ab.log, one process,
+//    slab / one-per-CU / two-per-CU): 3072 x 2560 x 4096 NN 130.3 / 136.1 /
+//    133.2, NT 129.0 / 134.7 / 133.1, TN 129.7 / 138.4 / 133.5; 2560^2 x 8192
+//    even (124.7 all, NT 115.4 all).
 //  * 64 x 64 ring with 32-deep K-tiles (8 KiB images), four workgroups per CU
 //    ("65" below), on every grid of 64-tiles since it beats both (one process,
 //    profiles/r05ah_f32_ring65_ab.log): 1536 x 2048^2 NN / TN / NT / TT 127 / 129 /
@@ -635,7 +640,7 @@ bool t64_tiles(i64 m, i64 n, i64 k) {
 // one-per-CU 128 x 128 ring and bit 3 the two-per-CU one on every grid of
 // 128-tiles, bit 1 the one-per-CU 64 x 64 ring and bit 2 the four-per-CU one on
 // grids of 64-tiles (both set: the first on grids of <= 256 64-tiles), 0 none.
-int ring_bt(bool kca, bool kcb, i64 m, i64 n, i64 k) {
+int ring_bt(i64 m, i64 n, i64 k) {
     const char* e = getenv("ELX_F32G_RING");
     if (t64_tiles(m, n, k)) {
         const int v = e ? atoi(e) : 4;
@@ -657,7 +662,7 @@ hipError_t launch_fb(const FParams& p, hipStream_t s) {
     // profiles/r03_f32_wtm.log)
     static const int wtm_env = [] { const char* v = getenv("ELX_F32G_WTM"); return v ? atoi(v) : 0; }();
     const int wtm = wtm_env ? wtm_env : (KCA && KCB && p.kchunk >= 32768) ? 64 : 32;
-    const int bt = ring_bt(KCA, KCB, p.m, p.n, p.k);
+    const int bt = ring_bt(p.m, p.n, p.k);
     if (bt == 128 && p.k % 64 == 0 && p.kchunk % 64 == 0) return launch_fr<128, 32768, KCA, KCB>(p, s);
     if (bt == 64 && p.k % 128 == 0 && p.kchunk % 128 == 0) return launch_fr<64, 32768, KCA, KCB>(p, s);
     if (bt == 65 && p.k % 32 == 0 && p.kchunk % 32 == 0) return launch_fr<64, 8192, KCA, KCB>(p, s);
@@ -691,7 +696,7 @@ DmaPlan gemm_f32_lds_dma_plan(bool ta, bool tb, i64 m, i64 n, i64 k, const float
     const bool kca = ta, kcb = !tb;
     const bool ok = k >= BK && al16(A) && al16(B) && lda % 4 == 0 && ldb % 4 == 0 && (kca || (m % 4 == 0 && m >= 4)) &&
                     (kcb || (n % 4 == 0 && n >= 4)) && m < (1ll << 31) && n < (1ll << 31);
-    const int bt = ring_bt(kca, kcb, m, n, k);
+    const int bt = ring_bt(m, n, k);
     if (bt == 65) return dma_plan(ok && k >= 32, (m + 63) / 64 * ((n + 63) / 64), k, 32, 1024);
     if (bt == 129) return dma_plan(ok && k >= 32, (m + 127) / 128 * ((n + 127) / 128), k, 32, 512);
     if (bt) {  // one workgroup per CU, K-tiles of 8192 / bt

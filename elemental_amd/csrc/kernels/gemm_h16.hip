@@ -108,15 +108,23 @@ __device__ __forceinline__ void tile_of_sb(int bid, int tiles_n, int xr, int pr,
 // so the two chunks of a 32-B column pair stay adjacent.
 __device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int swz_rc(int kk) { return ((kk & 3) << 1) | (((kk >> 3) & 1) << 3); }
+// RC images of 64-column blocks (the last block of a 192-row tile): 8 chunks per
+// 128-B k-row, k-row kk -> c ^ (2((kk>>1)&1) + 4((kk>>3)&1)).  A 32-lane half of
+// ds_read_b64_tr_b16 touches k-rows b + {0,1,2,3,8,9,10,11} (b a multiple of 4),
+// 32 B each; a 128-B pitch puts odd k-rows in the upper half of a 256-B bank row,
+// and within each parity the four k-rows get the four even XOR values, so the 16
+// chunk slots are distinct.
+__device__ __forceinline__ int swz_rc8(int kk) { return (((kk >> 1) & 1) << 1) | (((kk >> 3) & 1) << 2); }
 
 __device__ __forceinline__ void glds16(const uint16_t* src, lds_char* dst) {
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
 // One MFMA operand fragment (16 operand rows from R0, k-step s of 32):
-// lane l holds X(R0 + (l&15), 32s + 8(l>>4) + j), j = 0..7.
+// lane l holds X(R0 + (l&15), 32s + 8(l>>4) + j), j = 0..7.  RC: `narrow`
+// selects a 64-column block (128-B k-rows, swz_rc8) instead of a 128-column one.
 template <bool KC>
-__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l) {
+__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l, bool narrow = false) {
     if (KC) {
         const int row = R0 + (l & 15), c = 4 * s + (l >> 4);
         return *(const __attribute__((address_space(3))) u32x4*)(img + row * 128 + ((c ^ swz_kc(row)) << 4));
@@ -127,7 +135,8 @@ __device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int kk = 32 * s + 8 * g + 4 * h + q;
-            const lds_char* a = img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3);
+            const lds_char* a = narrow ? img + kk * 128 + ((c ^ swz_rc8(kk)) << 4) + ((p & 1) << 3)
+                                       : img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3);
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
             const u32x2 u = __builtin_bit_cast(u32x2, v);
             out[2 * h] = u[0];
@@ -232,12 +241,18 @@ template <int WM> struct Geo {
     static constexpr int BM = 32 * WM;           // tile edge (rows of op(A), columns of op(B))
     static constexpr int UNIT = BM * BK * 2;     // one operand's K-tile image
     static constexpr int WROWS = 16 * WM;        // operand rows one wave reads
+    // RC images: BM / 128 blocks of 128 columns (256-B k-rows, HALF bytes each),
+    // then one block of 64 columns (128-B k-rows) when BM = 128 q + 64 (WM = 6)
+    static constexpr int RCFULL = BM / 128;
+    static constexpr bool RCPART = BM % 128 != 0;
+    static_assert(BM % 128 == 0 || BM % 128 == 64, "RC images take 128- and 64-column blocks");
 };
 
 // per-lane offset (elements from the image's corner at k0) of piece j of one
 // operand's K-tile image, as the image is laid out: KC rows 8j..8j+7 (128 B
-// each), RC k-rows 4(j & 15)..+3 of the 128-row half j >> 4
-template <bool KC>
+// each); RC k-rows 4(j & 15)..+3 of the 128-column block j >> 4, or, in a
+// 64-column last block (WM = 6), k-rows 8i..8i+7 of it (i = j - 16 RCFULL)
+template <int WM, bool KC>
 __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld) {
     const int h = j >> 4, ins = j & 15;
     if (KC) {
@@ -247,9 +262,17 @@ __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld)
         const i64 row = R0 + row0 < rows ? row0 : rows - 1 - R0;
         return row * ld + 8 * c;
     } else {
-        const int kk = ins * 4 + (l >> 4);
-        const int c = (l & 15) ^ swz_rc(kk);
-        const i64 col0 = h * 128 + 8 * c;
+        int kk, c;
+        i64 col0;
+        if (Geo<WM>::RCPART && j >= 16 * Geo<WM>::RCFULL) {
+            kk = (j - 16 * Geo<WM>::RCFULL) * 8 + (l >> 3);
+            c = (l & 7) ^ swz_rc8(kk);
+            col0 = 128 * Geo<WM>::RCFULL + 8 * c;
+        } else {
+            kk = ins * 4 + (l >> 4);
+            c = (l & 15) ^ swz_rc(kk);
+            col0 = h * 128 + 8 * c;
+        }
         const i64 col = R0 + col0 <= rows - 8 ? col0 : rows - 8 - R0;
         return col + kk * ld;
     }
@@ -273,13 +296,15 @@ __device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0,
 }
 
 // a wave's operand fragment f (16 rows) of k-step s: KC images are one block of
-// 128-B rows; RC images are 128-row halves, so a wave's rows may start inside one
+// 128-B rows; RC images are 128-column blocks (and a last 64-column one at
+// WM = 6), so a wave's rows may start inside one
 template <int WM, bool KC>
 __device__ __forceinline__ u32x4 wfrag(const lds_char* img, int w_r, int f, int s, int l) {
     constexpr int WR = Geo<WM>::WROWS;
     const int r0 = w_r * WR + f * 16;
     if constexpr (KC) return frag<true>(img, r0, s, l);
-    else return frag<false>(img + (r0 >> 7) * HALF, r0 & 127, s, l);
+    else return frag<false>(img + (r0 >> 7) * HALF, r0 & 127, s, l,
+                            Geo<WM>::RCPART && (r0 >> 7) == Geo<WM>::RCFULL);
 }
 
 template <int WM>
@@ -435,7 +460,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 // SWP: B is the operand of the even units (staged first in a K-tile, one k-step
 // more DMA lead), A of the odd ones.
 template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART, bool SWP = false>
-__global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
+__global__ __launch_bounds__(256, WM >= 6 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
     constexpr int BMR = Geo<WM>::BM, UNIT = Geo<WM>::UNIT;
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
@@ -459,8 +484,8 @@ __global__ __launch_bounds__(256, WM == 8 ? 1 : 2) void gemm_h4w_kernel(H2Params
     Pieces<WM> pc;
 #pragma unroll
     for (int u = 0; u < WM; ++u) {
-        pc.gA[u] = piece_off<KCA>(w + 4 * u, l, m0, p.m, p.lda);
-        pc.gB[u] = piece_off<KCB>(w + 4 * u, l, n0, p.n, p.ldb);
+        pc.gA[u] = piece_off<WM, KCA>(w + 4 * u, l, m0, p.m, p.lda);
+        pc.gB[u] = piece_off<WM, KCB>(w + 4 * u, l, n0, p.n, p.ldb);
         pc.offA[u] = (int)(pc.gA[u] * 2);
         pc.offB[u] = (int)(pc.gB[u] * 2);
     }
@@ -592,46 +617,7 @@ int GroupM() {
 
 }  // namespace
 
-// Tile size and split-k of the four-wave kernel (kernels.hpp).
-//  * 256 x 256 tiles (WM = 8) unless fewer than half the CUs would get one;
-//    then 128 x 128 tiles (WM = 4, two workgroups per CU), a grid four times as
-//    wide.  In one process against the 256-tiles (profiles/r05b_h16_sweep.log):
-//    bf16 2048^3 382 -> 673 TF (hipBLASLt 659), 2560^3 (100 tiles) 542 -> 810,
-//    1536 x 2048^2 217 -> 528, 1024^3 69 -> 177, 1024^2 x 8192 347 -> 486 (with
-//    split-k), 2048^2 x 8192 873 -> 998; but 3072^3 (144 tiles) 834 -> 768 and
-//    4096^3 (256) 1309 -> 1139: where 256-tiles fill half the chip or more, their
-//    halved LDS reads per FLOP win.  ELX_H16_TILE = 256 / 128 forces one (read
-//    per call, for A/B).
-//  * split-k where the tiles still leave at least three quarters of the CUs
-//    idle: chunks of >= 4 K-tiles (16 at 64 tiles), up to one workgroup per CU;
-//    f32 partials in the stream-ordered workspace, one reduce that applies
-//    alpha / beta and rounds once.  Round 4 with 256-tiles: bf16 1024^2 x 8192 41
-//    -> 350 TF, 2048^2 x 8192 481 -> 866; at 2560^2 (100 tiles) three chunks lost
-//    22 % and at 3072^2 (144) two lost 35 % (profiles/r04_h16_split_ab.log,
-//    r04_h16_split_ab2.log, r04_h16_split_cap_ab.log).  ELX_H16_SPLIT = z caps the
-//    chunk count (0 or 1: none).
-H16Plan h16_plan(i64 m, i64 n, i64 kmain) {
-    const char* tv = getenv("ELX_H16_TILE");
-    const int force = tv ? atoi(tv) : 0;
-    const i64 t8 = ((m + 255) / 256) * ((n + 255) / 256);
-    H16Plan pl;
-    pl.wm = force == 128 ? 4 : force == 256 ? 8 : (t8 >= 128 ? 8 : 4);
-    const i64 bm = pl.wm * 32;
-    const i64 tiles = ((m + bm - 1) / bm) * ((n + bm - 1) / bm);
-    const char* sv = getenv("ELX_H16_SPLIT");
-    const i64 split_cap = sv ? (i64)atoi(sv) : 64;
-    pl.nz = 1;
-    pl.kchunk = kmain;
-    if (split_cap > 1 && tiles <= 64 && kmain >= 8 * BK) {
-        const i64 min_kt = tiles >= 64 ? 16 : 4;
-        const i64 z = std::min<i64>(std::min<i64>((256 + tiles - 1) / tiles, kmain / (min_kt * BK)), split_cap);
-        if (z >= 2) {
-            pl.kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
-            pl.nz = (kmain + pl.kchunk - 1) / pl.kchunk;
-        }
-    }
-    return pl;
-}
+// Tile size and split-k of the four-wave kernel: h16_plan in kernels.hpp.
 
 #ifndef ELX_KERNEL_PROBE
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
@@ -670,6 +656,8 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     }
     const int sbr = xr * pr, sbc = (8 / xr) * (32 / pr);
     const int mode = sbv ? atoi(sbv) : ((i64)tm_ * tn_ <= 4096 ? 1 : 0);
+    // (192-tiles measured even to +1 % in the grouped order: 3072^3 NN 1080 ->
+    // 1089, 6144^3 1305 -> 1315, profiles/r06c_h16_tile192_sweep.log)
     const int sblock = mode == 1 && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, tm_, tn_,
                (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), sblock, xr, pr, pl.kchunk,
@@ -680,7 +668,9 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
         e = workspace_alloc(reinterpret_cast<void**>(&p.W), sizeof(float) * (size_t)m * (size_t)n * (size_t)nz, s);
         if (e != hipSuccess) return e;
     }
-    e = pl.wm == 8 ? launch_h16_all<8>(is_bf16, kca, kcb, p, s) : launch_h16_all<4>(is_bf16, kca, kcb, p, s);
+    e = pl.wm == 8   ? launch_h16_all<8>(is_bf16, kca, kcb, p, s)
+        : pl.wm == 6 ? launch_h16_all<6>(is_bf16, kca, kcb, p, s)
+                     : launch_h16_all<4>(is_bf16, kca, kcb, p, s);
     if (nz > 1) {
         if (e == hipSuccess) {
             const i64 mn = m * n;

@@ -1,6 +1,7 @@
 // Host-side launch interface of the gfx950 kernels (no exceptions; return hipError_t).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -102,7 +103,63 @@ hipError_t gemm_f32_lds_dma(bool ta, bool tb, i64 m, i64 n, i64 kmain, i64 kchun
 // the 16-bit four-wave kernel's plan (gemm_h16.hip): tile 32 wm (wm 8 or 4),
 // nz split-k chunks of kchunk (nz = 1: whole k)
 struct H16Plan { int wm; i64 nz, kchunk; };
-H16Plan h16_plan(i64 m, i64 n, i64 kmain);
+// Tile size and split-k of the four-wave kernel (gemm_h16.hip; host-only, here
+// so tests/cpp/test_tile_rule.cpp checks it without a GPU).
+//  * 256 x 256 tiles (WM = 8) unless fewer than half the CUs would get one;
+//    then 128 x 128 tiles (WM = 4, two workgroups per CU), a grid four times as
+//    wide.  In one process against the 256-tiles (profiles/r05b_h16_sweep.log):
+//    bf16 2048^3 382 -> 673 TF (hipBLASLt 659), 2560^3 (100 tiles) 542 -> 810,
+//    1536 x 2048^2 217 -> 528, 1024^3 69 -> 177, 1024^2 x 8192 347 -> 486 (with
+//    split-k), 2048^2 x 8192 873 -> 998; but 3072^3 (144 tiles) 834 -> 768 and
+//    4096^3 (256) 1309 -> 1139: where 256-tiles fill half the chip or more, their
+//    halved LDS reads per FLOP win.
+//  * 192 x 192 tiles (WM = 6, one workgroup per CU, round 6) where they fill the
+//    CUs' rounds clearly better than 256-tiles: a last round of 256-tiles that
+//    leaves the chip a quarter or more emptier (utilisation u = tiles / (rounds x
+//    256) at least 1.25x u8), or, in the 128-tile range, at least 192 of them
+//    (three quarters of the CUs in one round).  Measured in one process beside
+//    hipBLASLt (profiles/r06c_h16_tile192_sweep.log, r06d_h16_tile_map.log; bf16
+//    NN, 256 / 192 / 128 / vendor): 3072^3 (144 / 256 / 576 tiles) 830 / 1094 /
+//    767 / 973 TF (TN / NT / TT 1107 / 1070 / 1087, vendor 993 / 875 / 1031; f16
+//    1065 vs 900), 6144^3 1161 / 1294 / 1114 / 1249, 3072^2 x 12288 1123 / 1411
+//    / 910 / 1174, 2560^2 x 8192 743 / 1057 / 879 / 1032; where the 256-tiles'
+//    rounds are nearly full they win (4096^3 1285 / 1096 / 1107, 5120^3 1204 /
+//    1153, 7168^3 1157 / 1093, 12288^3 1443 / 1140: the smaller tile reads a
+//    third more operand bytes per FLOP, which costs once the operands outgrow
+//    the Infinity Cache).  ELX_H16_TILE = 256 / 192 / 128 forces one (read per
+//    call, for A/B).
+inline H16Plan h16_plan(i64 m, i64 n, i64 kmain) {
+    constexpr i64 BK = 64;  // the four-wave kernel's K-tile
+    const char* tv = getenv("ELX_H16_TILE");
+    const int force = tv ? atoi(tv) : 0;
+    auto tiles_of = [&](i64 bm) { return ((m + bm - 1) / bm) * ((n + bm - 1) / bm); };
+    auto util = [](i64 t) { return (double)t / (double)(((t + 255) / 256) * 256); };
+    const i64 t8 = tiles_of(256), t6 = tiles_of(192);
+    H16Plan pl;
+    if (force == 128 || force == 192 || force == 256) {
+        pl.wm = force / 32;
+    } else if (t8 >= 128) {
+        pl.wm = util(t6) >= 1.25 * util(t8) ? 6 : 8;
+    } else {
+        pl.wm = t6 >= 192 ? 6 : 4;
+    }
+    const i64 bm = pl.wm * 32;
+    const i64 tiles = ((m + bm - 1) / bm) * ((n + bm - 1) / bm);
+    const char* sv = getenv("ELX_H16_SPLIT");
+    const i64 split_cap = sv ? (i64)atoi(sv) : 64;
+    pl.nz = 1;
+    pl.kchunk = kmain;
+    if (split_cap > 1 && tiles <= 64 && kmain >= 8 * BK) {
+        const i64 min_kt = tiles >= 64 ? 16 : 4;
+        const i64 z = std::min<i64>(std::min<i64>((256 + tiles - 1) / tiles, kmain / (min_kt * BK)), split_cap);
+        if (z >= 2) {
+            pl.kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
+            pl.nz = (kmain + pl.kchunk - 1) / pl.kchunk;
+        }
+    }
+    return pl;
+}
+
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha,
                        const uint16_t* A, i64 lda, const uint16_t* B, i64 ldb, float beta,
                        uint16_t* C, i64 ldc, hipStream_t s);

@@ -45,6 +45,25 @@ int main() {
     if (!few.use || few.nz != 4 || few.kchunk * few.nz < few.kmain) { std::printf("FAIL plan 64 tiles: nz %d\n", few.nz); ++bad; }
     const elx::kern::DmaPlan t64 = elx::kern::dma_plan(true, 256, 2048, 16);  // 1024^2 in 64-tiles
     if (!t64.use || t64.nz != 1) { std::printf("FAIL plan 256 tiles: nz %d\n", t64.nz); ++bad; }
+    // the 16-bit four-wave kernel's tile (h16_plan): 256 / 192 / 128 by the
+    // round-6 map (profiles/r06d_h16_tile_map.log, r06c_h16_tile192_sweep.log)
+    struct H { i64 m, n, k; int wm; };
+    const H hc[] = {
+        {3072, 3072, 3072, 6},   {6144, 6144, 6144, 6},   {3072, 3072, 12288, 6}, {2560, 2560, 8192, 6},
+        {2560, 2560, 2560, 6},   {3584, 3584, 3584, 8},   {4096, 4096, 4096, 8},  {4608, 4608, 4608, 8},
+        {5120, 5120, 5120, 8},   {7168, 7168, 7168, 8},   {12288, 12288, 12288, 8}, {32768, 32768, 32768, 8},
+        {16384, 8192, 8192, 8},  {2048, 2048, 2048, 4},   {1536, 2048, 2048, 4},  {1024, 1024, 8192, 4},
+    };
+    for (const H& c : hc) {
+        const elx::kern::H16Plan pl = elx::kern::h16_plan(c.m, c.n, c.k);
+        if (pl.wm != c.wm) {
+            std::printf("FAIL h16_plan %lld x %lld x %lld: wm %d want %d\n", (long long)c.m, (long long)c.n,
+                        (long long)c.k, pl.wm, c.wm);
+            ++bad;
+        }
+    }
+    const elx::kern::H16Plan sk = elx::kern::h16_plan(1024, 1024, 8192);  // 64 128-tiles: split k
+    if (sk.nz < 2 || sk.kchunk * sk.nz < 8192) { std::printf("FAIL h16 split 1024^2 x 8192: nz %lld\n", (long long)sk.nz); ++bad; }
     std::printf("%s (%d failures)\n", bad ? "FAILED" : "ok", bad);
     return bad ? 1 : 0;
 }
