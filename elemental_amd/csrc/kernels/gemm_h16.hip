@@ -115,6 +115,11 @@ __device__ __forceinline__ int swz_rc(int kk) { return ((kk & 3) << 1) | (((kk >
 // and within each parity the four k-rows get the four even XOR values, so the 16
 // chunk slots are distinct.
 __device__ __forceinline__ int swz_rc8(int kk) { return (((kk >> 1) & 1) << 1) | (((kk >> 3) & 1) << 2); }
+// RC images of 32-column blocks (the last block of a 160- or 224-row tile): 4
+// chunks per 64-B k-row, k-row kk -> c ^ 2((kk>>3)&1).  The same half-wave's
+// eight k-rows fall four to a bank row (kk & 3 picks the 64-B quarter), and the
+// two that share a quarter (kk, kk + 8) get different chunk pairs.
+__device__ __forceinline__ int swz_rc4(int kk) { return ((kk >> 3) & 1) << 1; }
 
 __device__ __forceinline__ void glds16(const uint16_t* src, lds_char* dst) {
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
@@ -122,9 +127,10 @@ __device__ __forceinline__ void glds16(const uint16_t* src, lds_char* dst) {
 
 // One MFMA operand fragment (16 operand rows from R0, k-step s of 32):
 // lane l holds X(R0 + (l&15), 32s + 8(l>>4) + j), j = 0..7.  RC: `narrow`
-// selects a 64-column block (128-B k-rows, swz_rc8) instead of a 128-column one.
+// selects the block kind: 0 = 128 columns (256-B k-rows, swz_rc), 1 = 64
+// columns (128-B k-rows, swz_rc8), 2 = 32 columns (64-B k-rows, swz_rc4).
 template <bool KC>
-__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l, bool narrow = false) {
+__device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l, int narrow = 0) {
     if (KC) {
         const int row = R0 + (l & 15), c = 4 * s + (l >> 4);
         return *(const __attribute__((address_space(3))) u32x4*)(img + row * 128 + ((c ^ swz_kc(row)) << 4));
@@ -135,8 +141,9 @@ __device__ __forceinline__ u32x4 frag(const lds_char* img, int R0, int s, int l,
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int kk = 32 * s + 8 * g + 4 * h + q;
-            const lds_char* a = narrow ? img + kk * 128 + ((c ^ swz_rc8(kk)) << 4) + ((p & 1) << 3)
-                                       : img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3);
+            const lds_char* a = narrow == 0   ? img + kk * 256 + ((c ^ swz_rc(kk)) << 4) + ((p & 1) << 3)
+                                : narrow == 1 ? img + kk * 128 + ((c ^ swz_rc8(kk)) << 4) + ((p & 1) << 3)
+                                              : img + kk * 64 + ((c ^ swz_rc4(kk)) << 4) + ((p & 1) << 3);
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
             const u32x2 u = __builtin_bit_cast(u32x2, v);
             out[2 * h] = u[0];
@@ -241,11 +248,15 @@ template <int WM> struct Geo {
     static constexpr int BM = 32 * WM;           // tile edge (rows of op(A), columns of op(B))
     static constexpr int UNIT = BM * BK * 2;     // one operand's K-tile image
     static constexpr int WROWS = 16 * WM;        // operand rows one wave reads
-    // RC images: BM / 128 blocks of 128 columns (256-B k-rows, HALF bytes each),
-    // then one block of 64 columns (128-B k-rows) when BM = 128 q + 64 (WM = 6)
+    // RC images: BM / 128 blocks of 128 columns (256-B k-rows, HALF bytes
+    // each), then a block of 64 columns (128-B k-rows, 8 KiB) if BM % 128 >= 64,
+    // then one of 32 columns (64-B k-rows, 4 KiB) if BM % 64 == 32: WM 8 / 4 =
+    // 128-blocks only, WM 6 = 128 + 64, WM 5 = 128 + 32, WM 7 = 128 + 64 + 32
     static constexpr int RCFULL = BM / 128;
-    static constexpr bool RCPART = BM % 128 != 0;
-    static_assert(BM % 128 == 0 || BM % 128 == 64, "RC images take 128- and 64-column blocks");
+    static constexpr bool RC64 = (BM % 128) >= 64, RC32 = (BM % 64) == 32;
+    static constexpr int C64 = 128 * RCFULL, C32 = C64 + (RC64 ? 64 : 0);       // first column of each
+    static constexpr int J64 = 16 * RCFULL, J32 = J64 + (RC64 ? 8 : 0);          // first piece of each
+    static constexpr int O64 = RCFULL * HALF, O32 = O64 + (RC64 ? HALF / 2 : 0);  // byte offset of each
 };
 
 // per-lane offset (elements from the image's corner at k0) of piece j of one
@@ -262,12 +273,17 @@ __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld)
         const i64 row = R0 + row0 < rows ? row0 : rows - 1 - R0;
         return row * ld + 8 * c;
     } else {
+        using G = Geo<WM>;
         int kk, c;
         i64 col0;
-        if (Geo<WM>::RCPART && j >= 16 * Geo<WM>::RCFULL) {
-            kk = (j - 16 * Geo<WM>::RCFULL) * 8 + (l >> 3);
+        if (G::RC32 && j >= G::J32) {  // 32-column block: 16 k-rows x 64 B per piece
+            kk = (j - G::J32) * 16 + (l >> 2);
+            c = (l & 3) ^ swz_rc4(kk);
+            col0 = G::C32 + 8 * c;
+        } else if (G::RC64 && j >= G::J64) {  // 64-column block: 8 k-rows x 128 B
+            kk = (j - G::J64) * 8 + (l >> 3);
             c = (l & 7) ^ swz_rc8(kk);
-            col0 = 128 * Geo<WM>::RCFULL + 8 * c;
+            col0 = G::C64 + 8 * c;
         } else {
             kk = ins * 4 + (l >> 4);
             c = (l & 15) ^ swz_rc(kk);
@@ -302,9 +318,14 @@ template <int WM, bool KC>
 __device__ __forceinline__ u32x4 wfrag(const lds_char* img, int w_r, int f, int s, int l) {
     constexpr int WR = Geo<WM>::WROWS;
     const int r0 = w_r * WR + f * 16;
-    if constexpr (KC) return frag<true>(img, r0, s, l);
-    else return frag<false>(img + (r0 >> 7) * HALF, r0 & 127, s, l,
-                            Geo<WM>::RCPART && (r0 >> 7) == Geo<WM>::RCFULL);
+    if constexpr (KC) {
+        return frag<true>(img, r0, s, l);
+    } else {
+        using G = Geo<WM>;
+        if (G::RC32 && r0 >= G::C32) return frag<false>(img + G::O32, r0 - G::C32, s, l, 2);
+        if (G::RC64 && r0 >= G::C64) return frag<false>(img + G::O64, r0 - G::C64, s, l, 1);
+        return frag<false>(img + (r0 >> 7) * HALF, r0 & 127, s, l, 0);
+    }
 }
 
 template <int WM>
@@ -441,7 +462,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
         mfma_acc<BF16>(acc[i / WM][i % WM], cur.a[i / WM], cur.b[i % WM]);
-        if (i >= NM / 2 && (i - NM / 2) % GAP == 1 % GAP) {
+        if (i >= NM / 2 && (i - NM / 2) % GAP == 1 % GAP && (i - NM / 2) / GAP < WM) {
             const int u = (i - NM / 2) / GAP;
             if constexpr (SB) piece<BMR, BUF, KCB>(p.B, p.ldb, n0, k0, pc.offB[u], pc.gB[u], w + 4 * u, st);
             else piece<BMR, BUF, KCA>(p.A, p.lda, m0, k0, pc.offA[u], pc.gA[u], w + 4 * u, st);
@@ -460,7 +481,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 // SWP: B is the operand of the even units (staged first in a K-tile, one k-step
 // more DMA lead), A of the odd ones.
 template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART, bool SWP = false>
-__global__ __launch_bounds__(256, WM >= 6 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
+__global__ __launch_bounds__(256, WM >= 5 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
     constexpr int BMR = Geo<WM>::BM, UNIT = Geo<WM>::UNIT;
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
@@ -624,7 +645,7 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
     const bool kca = ta, kcb = !tb;
     const i64 kmain = k / BK * BK;
-    const H16Plan pl = h16_plan(m, n, kmain);
+    const H16Plan pl = h16_plan(m, n, kmain, kca && kcb);
     const int BMR = pl.wm * 32;
     const i64 tiles = ((m + BMR - 1) / BMR) * ((n + BMR - 1) / BMR);
     // the LDS-DMA path: 16-B aligned rows/columns for the DMA, RC operands a
@@ -668,9 +689,13 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
         e = workspace_alloc(reinterpret_cast<void**>(&p.W), sizeof(float) * (size_t)m * (size_t)n * (size_t)nz, s);
         if (e != hipSuccess) return e;
     }
-    e = pl.wm == 8   ? launch_h16_all<8>(is_bf16, kca, kcb, p, s)
-        : pl.wm == 6 ? launch_h16_all<6>(is_bf16, kca, kcb, p, s)
-                     : launch_h16_all<4>(is_bf16, kca, kcb, p, s);
+    switch (pl.wm) {
+    case 8: e = launch_h16_all<8>(is_bf16, kca, kcb, p, s); break;
+    case 7: e = launch_h16_all<7>(is_bf16, kca, kcb, p, s); break;
+    case 6: e = launch_h16_all<6>(is_bf16, kca, kcb, p, s); break;
+    case 5: e = launch_h16_all<5>(is_bf16, kca, kcb, p, s); break;
+    default: e = launch_h16_all<4>(is_bf16, kca, kcb, p, s); break;
+    }
     if (nz > 1) {
         if (e == hipSuccess) {
             const i64 mn = m * n;

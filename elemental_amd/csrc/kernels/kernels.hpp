@@ -113,35 +113,57 @@ struct H16Plan { int wm; i64 nz, kchunk; };
 //    split-k), 2048^2 x 8192 873 -> 998; but 3072^3 (144 tiles) 834 -> 768 and
 //    4096^3 (256) 1309 -> 1139: where 256-tiles fill half the chip or more, their
 //    halved LDS reads per FLOP win.
-//  * 192 x 192 tiles (WM = 6, one workgroup per CU, round 6) where they fill the
-//    CUs' rounds clearly better than 256-tiles: a last round of 256-tiles that
-//    leaves the chip a quarter or more emptier (utilisation u = tiles / (rounds x
-//    256) at least 1.25x u8), or, in the 128-tile range, at least 192 of them
-//    (three quarters of the CUs in one round).  Measured in one process beside
-//    hipBLASLt (profiles/r06c_h16_tile192_sweep.log, r06d_h16_tile_map.log; bf16
-//    NN, 256 / 192 / 128 / vendor): 3072^3 (144 / 256 / 576 tiles) 830 / 1094 /
-//    767 / 973 TF (TN / NT / TT 1107 / 1070 / 1087, vendor 993 / 875 / 1031; f16
-//    1065 vs 900), 6144^3 1161 / 1294 / 1114 / 1249, 3072^2 x 12288 1123 / 1411
-//    / 910 / 1174, 2560^2 x 8192 743 / 1057 / 879 / 1032; where the 256-tiles'
-//    rounds are nearly full they win (4096^3 1285 / 1096 / 1107, 5120^3 1204 /
-//    1153, 7168^3 1157 / 1093, 12288^3 1443 / 1140: the smaller tile reads a
-//    third more operand bytes per FLOP, which costs once the operands outgrow
-//    the Infinity Cache).  ELX_H16_TILE = 256 / 192 / 128 forces one (read per
+//  * 192 x 192 tiles (WM = 6, one workgroup per CU, round 6) where the
+//    256-tiles leave more than a quarter of their last round's CUs idle
+//    (utilisation u8 = tiles / (rounds x 256) <= 0.75) and a round of 192-tiles
+//    fills clearly better, 128-tiles (two per CU, 512 slots per round) where
+//    they do: each candidate scored u x its measured relative rate (192 and
+//    128: 0.8 of the 256-tile loop at full rounds), the 256-tiles kept unless
+//    beaten.  Measured in one process beside hipBLASLt on two boxes
+//    (profiles/r06c_h16_tile192_sweep.log, r06d_h16_tile_map.log,
+//    r06e_h16_midsize_vs_vendor_b0.log, r06h_h16_tile_map_b0.log; bf16 NN,
+//    256 / 192 / 128 / vendor): 3072^3 (u8 0.56, u6 1.0) 830 / 1094 / 767 / 973
+//    and 896 / 1042 / 816 / 966; 4608^3 (u8 0.63, 128-tiles 0.84) 968 / 989 /
+//    1017 and 1015 / 897 / 1075; 4096 x 2048 x 4096 (u8 0.5, u4 1.0) 817 / 1014
+//    / 1090; 6144^3 (u8 0.75) 1161 / 1294 / 1114 and 1212 / 1195 / 1179: the
+//    192-tile's rate varies more between boxes (it reads a third more operand
+//    bytes per FLOP than the 256-tile).  Below 128 256-tiles the 128-tiles
+//    stay (2560^3: 128-tiles 856 / 880 against 834 / 710 for 192), except for
+//    TN grids of nearly a full round of 160-tiles (below).
+//  * TN (both operands k-contiguous) may also take 224 x 224 (WM = 7) and
+//    160 x 160 (WM = 5) tiles, rated 0.92 and 0.8: TN 3584^3 (16 x 16 224-tiles)
+//    1209 -> 1320 TF (hipBLASLt 1358), TN 2560^3 (16 x 16 160-tiles) 863 -> 999
+//    (980).  With a rows-contiguous operand they lose (NN 3584^3 224-tiles 1074
+//    vs 1181: their last RC block is 32 columns, 64-B k-rows, twice the DMA
+//    requests per byte of the 128-column blocks), so other orientations never
+//    take them.  ELX_H16_TILE = 256 / 224 / 192 / 160 / 128 forces one (read per
 //    call, for A/B).
-inline H16Plan h16_plan(i64 m, i64 n, i64 kmain) {
+inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
     constexpr i64 BK = 64;  // the four-wave kernel's K-tile
     const char* tv = getenv("ELX_H16_TILE");
     const int force = tv ? atoi(tv) : 0;
     auto tiles_of = [&](i64 bm) { return ((m + bm - 1) / bm) * ((n + bm - 1) / bm); };
-    auto util = [](i64 t) { return (double)t / (double)(((t + 255) / 256) * 256); };
-    const i64 t8 = tiles_of(256), t6 = tiles_of(192);
+    auto util = [](i64 t, i64 slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
     H16Plan pl;
-    if (force == 128 || force == 192 || force == 256) {
+    if (force == 128 || force == 160 || force == 192 || force == 224 || force == 256) {
         pl.wm = force / 32;
-    } else if (t8 >= 128) {
-        pl.wm = util(t6) >= 1.25 * util(t8) ? 6 : 8;
+    } else if (tiles_of(256) < 128) {
+        pl.wm = tn && tiles_of(160) >= 224 ? 5 : 4;
     } else {
-        pl.wm = t6 >= 192 ? 6 : 4;
+        const double u8 = util(tiles_of(256), 256);
+        pl.wm = 8;
+        if (u8 <= 0.75) {
+            double best = u8;
+            const double s6 = 0.8 * util(tiles_of(192), 256), s4 = 0.8 * util(tiles_of(128), 512);
+            if (s6 > best) { best = s6; pl.wm = 6; }
+            if (s4 > best) { best = s4; pl.wm = 4; }
+        }
+        if (tn && u8 < 1.0) {
+            double best = pl.wm == 8 ? u8 : pl.wm == 6 ? 0.8 * util(tiles_of(192), 256) : 0.8 * util(tiles_of(128), 512);
+            const double s7 = 0.92 * util(tiles_of(224), 256), s5 = 0.8 * util(tiles_of(160), 256);
+            if (s7 > best) { best = s7; pl.wm = 7; }
+            if (s5 > best) { best = s5; pl.wm = 5; }
+        }
     }
     const i64 bm = pl.wm * 32;
     const i64 tiles = ((m + bm - 1) / bm) * ((n + bm - 1) / bm);

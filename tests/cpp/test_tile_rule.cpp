@@ -47,18 +47,23 @@ int main() {
     if (!t64.use || t64.nz != 1) { std::printf("FAIL plan 256 tiles: nz %d\n", t64.nz); ++bad; }
     // the 16-bit four-wave kernel's tile (h16_plan): 256 / 192 / 128 by the
     // round-6 map (profiles/r06d_h16_tile_map.log, r06c_h16_tile192_sweep.log)
-    struct H { i64 m, n, k; int wm; };
+    struct H { i64 m, n, k; int wm; bool tn; };
     const H hc[] = {
-        {3072, 3072, 3072, 6},   {6144, 6144, 6144, 6},   {3072, 3072, 12288, 6}, {2560, 2560, 8192, 6},
-        {2560, 2560, 2560, 6},   {3584, 3584, 3584, 8},   {4096, 4096, 4096, 8},  {4608, 4608, 4608, 8},
-        {5120, 5120, 5120, 8},   {7168, 7168, 7168, 8},   {12288, 12288, 12288, 8}, {32768, 32768, 32768, 8},
-        {16384, 8192, 8192, 8},  {2048, 2048, 2048, 4},   {1536, 2048, 2048, 4},  {1024, 1024, 8192, 4},
+        {3072, 3072, 3072, 6, false},   {6144, 6144, 6144, 6, false},   {3072, 3072, 12288, 6, false},
+        {2560, 2560, 8192, 4, false},   {2560, 2560, 2560, 4, false},   {3584, 3584, 3584, 8, false},
+        {4096, 4096, 4096, 8, false},   {4608, 4608, 4608, 4, false},   {5120, 5120, 5120, 8, false},
+        {7168, 7168, 7168, 8, false},   {12288, 12288, 12288, 8, false}, {32768, 32768, 32768, 8, false},
+        {16384, 8192, 8192, 8, false},  {2048, 2048, 2048, 4, false},   {1536, 2048, 2048, 4, false},
+        {1024, 1024, 8192, 4, false},   {4096, 2048, 4096, 4, false},   {8192, 4096, 2048, 8, false},
+        // TN may take the 224- and 160-tiles
+        {3584, 3584, 3584, 7, true},    {2560, 2560, 2560, 5, true},    {3072, 3072, 3072, 6, true},
+        {4096, 4096, 4096, 8, true},    {16384, 16384, 16384, 8, true}, {2048, 2048, 2048, 4, true},
     };
     for (const H& c : hc) {
-        const elx::kern::H16Plan pl = elx::kern::h16_plan(c.m, c.n, c.k);
+        const elx::kern::H16Plan pl = elx::kern::h16_plan(c.m, c.n, c.k, c.tn);
         if (pl.wm != c.wm) {
-            std::printf("FAIL h16_plan %lld x %lld x %lld: wm %d want %d\n", (long long)c.m, (long long)c.n,
-                        (long long)c.k, pl.wm, c.wm);
+            std::printf("FAIL h16_plan %lld x %lld x %lld%s: wm %d want %d\n", (long long)c.m, (long long)c.n,
+                        (long long)c.k, c.tn ? " TN" : "", pl.wm, c.wm);
             ++bad;
         }
     }

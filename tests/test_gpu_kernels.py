@@ -317,13 +317,13 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
     assert bad.size == 0, f"{kind} alpha={alpha} beta={beta}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
-@pytest.mark.parametrize("tile", ["", "128", "192", "256", "g"])
+@pytest.mark.parametrize("tile", ["", "128", "160", "192", "224", "256", "g"])
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64), (1024, 1024, 8192),
                                    (1002, 1032, 4096), (2048, 2048, 2112), (1536, 2312, 704), (4096, 4096, 192),
-                                   (3072, 3072, 192)])
+                                   (3072, 3072, 192), (2560, 2560, 192), (3584, 3584, 128)])
 def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     """Integer operands in [-2, 2]: every partial sum is exact in the f32
     accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
@@ -336,10 +336,12 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     tiles, (1024, 1024, 8192) 16, (1002, 1032, 4096) 13 with m % 4 != 0 (the
     partials' scalar stores; TN / TT only, the others take the simple kernel).
     `tile`: the four-wave kernel's tile as the plan picks it (""), or forced to
-    128 x 128 / 192 x 192 / 256 x 256 (ELX_H16_TILE), so every instantiation
-    sees every shape (192: rows-contiguous images in a 128- and a 64-column
-    block).  (4096, 4096, 192) / (3072, 3072, 192): 16 x 16 grids of 256- /
-    192-tiles, run in the super-block tile order (tile_of_sb).  (k a multiple of 64: a k tail is a
+    128 / 160 / 192 / 224 / 256 (ELX_H16_TILE), so every instantiation sees
+    every shape (rows-contiguous images in 128-column blocks plus a 64- and / or
+    a 32-column block: 192 = 128 + 64, 160 = 128 + 32, 224 = 128 + 64 + 32).
+    (4096, 4096, 192) / (3072, 3072, 192) / (2560, 2560, 192) / (3584, 3584,
+    128): 16 x 16 grids of 256- / 192- / 160- / 224-tiles (the 256-tiles' in the
+    super-block tile order, tile_of_sb).  (k a multiple of 64: a k tail is a
     second pass that adds to the already rounded C.)  tile = "g": the plan's
     tile with the DMA in its 64-bit-address form (ELX_H16_STAGE=g; operands too
     long for 31-bit buffer offsets take it)."""
