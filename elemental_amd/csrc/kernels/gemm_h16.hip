@@ -69,6 +69,9 @@ struct H2Params {
     // h16_splitk_reduce applies alpha / beta and rounds once
     i64 kchunk;
     float* W;
+    // > 0: launch only the first dp_tiles tiles of the tile order (the
+    // data-parallel rounds of gemm_mfma_h's tail split); 0: every tile
+    int dp_tiles;
 };
 
 __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
@@ -590,7 +593,8 @@ hipError_t launch_h16(const H2Params& p, hipStream_t s) {
     // (ELX_H16_STAGE=g, read per call, forces the global form: the tests cover it)
     const char* stg = getenv("ELX_H16_STAGE");
     const bool buf = !(stg && stg[0] == 'g') && dma_fits(KCA ? BMR : BK, p.lda, 2) && dma_fits(KCB ? BMR : BK, p.ldb, 2);
-    const dim3 grid(p.tiles_m * p.tiles_n, p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
+    const dim3 grid(p.dp_tiles > 0 ? p.dp_tiles : p.tiles_m * p.tiles_n,
+                    p.W ? (unsigned)((p.k + p.kchunk - 1) / p.kchunk) : 1u);
     // B's units first (SWP) except for NN, 256 x 256 tiles: one process, bf16
     // 16384^3 NN / NT / TN / TT 1523 / 1421 / 1514 / 1428 -> 1494 / 1459 / 1529 /
     // 1509 TF with B first, 32768^3 NN 1451 -> 1432, TT 1379 -> 1440
@@ -682,20 +686,57 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     const int sblock = mode == 1 && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, tm_, tn_,
                (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), sblock, xr, pr, pl.kchunk,
-               nullptr};
+               nullptr, 0};
     const i64 nz = pl.nz;
     hipError_t e;
+    auto launch = [&]() {
+        switch (pl.wm) {
+        case 8: return launch_h16_all<8>(is_bf16, kca, kcb, p, s);
+        case 7: return launch_h16_all<7>(is_bf16, kca, kcb, p, s);
+        case 6: return launch_h16_all<6>(is_bf16, kca, kcb, p, s);
+        case 5: return launch_h16_all<5>(is_bf16, kca, kcb, p, s);
+        default: return launch_h16_all<4>(is_bf16, kca, kcb, p, s);
+        }
+    };
+    // Data-parallel rounds + a tail of smaller tiles (round 6).  A grid whose
+    // last round holds at most a quarter of the slots (256 one-per-CU tiles,
+    // 512 two-per-CU 128-tiles) leaves most CUs idle for one whole tile's K.  The tiles
+    // of that round are the last ones of the grouped order: in the last group
+    // of tile rows, its last columns.  Rounded up to whole group columns they
+    // form one rectangle of C; the full rounds run as one launch over the
+    // first tiles of the order (dp_tiles), and the rectangle as its own GEMM,
+    // whose plan gives it tiles small enough (or split-k) to spread over the
+    // chip.  Every element of C is written by exactly one of the two, each
+    // rounding once.  In one process, tail on / off (profiles/
+    // r06j_h16_tail_split_ab.log, bf16 at beta 0; hipBLASLt): NN 7168^3 (784 =
+    // 3 x 256 + 16 256-tiles) 1226 -> 1423 TF (1165), 10240^3 (1600 = 6 x 256 +
+    // 64) 1322 -> 1375 (1280), 6144^3 in 256-tiles (576 = 2 x 256 + 64) 1231 ->
+    // 1290 (1285), TN 1263 -> 1328, 3072^2 x 4096 in 128-tiles (576 = 512 + 64)
+    // 864 -> 904; a last round of half the slots lost (6144 x 4096^2, 384 =
+    // 256 + 128: 1193 -> 1167), hence the quarter.  ELX_H16_TAIL = 0 turns it
+    // off (read per call, for A/B).
+    const char* tv = getenv("ELX_H16_TAIL");
+    const bool tail_on = !(tv && tv[0] == '0');
+    const i64 slots = pl.wm == 4 ? 512 : 256;
+    if (tail_on && nz == 1 && !sblock && kmain == k && k >= 1024 && tiles > slots) {
+        const i64 rem = tiles % slots;
+        const int G = p.group_m;
+        const int last = (tm_ - 1) / G, gsz = tm_ - last * G;  // the last group's tile rows
+        const i64 cols = (rem + gsz - 1) / gsz;                 // its tail columns
+        if (rem > 0 && rem <= slots / 4 && cols <= tn_) {
+            p.dp_tiles = (int)(tiles - cols * gsz);
+            e = launch();
+            if (e != hipSuccess) return e;
+            const i64 i0 = (i64)last * G * BMR, j0 = (tn_ - cols) * BMR;
+            return gemm_mfma_h(is_bf16, ta, tb, m - i0, n - j0, k, alpha, ta ? A + i0 * lda : A + i0, lda,
+                               tb ? B + j0 : B + j0 * ldb, ldb, beta, C + i0 + j0 * ldc, ldc, s);
+        }
+    }
     if (nz > 1) {
         e = workspace_alloc(reinterpret_cast<void**>(&p.W), sizeof(float) * (size_t)m * (size_t)n * (size_t)nz, s);
         if (e != hipSuccess) return e;
     }
-    switch (pl.wm) {
-    case 8: e = launch_h16_all<8>(is_bf16, kca, kcb, p, s); break;
-    case 7: e = launch_h16_all<7>(is_bf16, kca, kcb, p, s); break;
-    case 6: e = launch_h16_all<6>(is_bf16, kca, kcb, p, s); break;
-    case 5: e = launch_h16_all<5>(is_bf16, kca, kcb, p, s); break;
-    default: e = launch_h16_all<4>(is_bf16, kca, kcb, p, s); break;
-    }
+    e = launch();
     if (nz > 1) {
         if (e == hipSuccess) {
             const i64 mn = m * n;

@@ -127,7 +127,10 @@ struct H16Plan { int wm; i64 nz, kchunk; };
 //    1017 and 1015 / 897 / 1075; 4096 x 2048 x 4096 (u8 0.5, u4 1.0) 817 / 1014
 //    / 1090; 6144^3 (u8 0.75) 1161 / 1294 / 1114 and 1212 / 1195 / 1179: the
 //    192-tile's rate varies more between boxes (it reads a third more operand
-//    bytes per FLOP than the 256-tile).  Below 128 256-tiles the 128-tiles
+//    bytes per FLOP than the 256-tile).  A grid whose last round of 256-tiles
+//    is at most a quarter full counts as 0.95: gemm_mfma_h's tail split runs
+//    that round on smaller tiles (6144^3: 256-tiles with the tail 1290 TF, the
+//    192-tiles 1185 on the same box, profiles/r06j_h16_tail_split_ab.log).  Below 128 256-tiles the 128-tiles
 //    stay (2560^3: 128-tiles 856 / 880 against 834 / 710 for 192), except for
 //    TN grids of nearly a full round of 160-tiles (below).
 //  * TN (both operands k-contiguous) may also take 224 x 224 (WM = 7) and
@@ -150,7 +153,13 @@ inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
     } else if (tiles_of(256) < 128) {
         pl.wm = tn && tiles_of(160) >= 224 ? 5 : 4;
     } else {
-        const double u8 = util(tiles_of(256), 256);
+        // gemm_mfma_h runs a last round of at most a quarter of the slots as
+        // a separate GEMM on smaller tiles (the tail split): such a grid counts
+        // as nearly full
+        const char* tl = getenv("ELX_H16_TAIL");
+        const i64 t8 = tiles_of(256), r8 = t8 % 256;
+        const bool tail8 = !(tl && tl[0] == '0') && t8 > 256 && r8 > 0 && r8 <= 64 && kmain >= 1024;
+        const double u8 = tail8 ? 0.95 : util(t8, 256);
         pl.wm = 8;
         if (u8 <= 0.75) {
             double best = u8;

@@ -49,7 +49,7 @@ int main() {
     // round-6 map (profiles/r06d_h16_tile_map.log, r06c_h16_tile192_sweep.log)
     struct H { i64 m, n, k; int wm; bool tn; };
     const H hc[] = {
-        {3072, 3072, 3072, 6, false},   {6144, 6144, 6144, 6, false},   {3072, 3072, 12288, 6, false},
+        {3072, 3072, 3072, 6, false},   {6144, 6144, 6144, 8, false},   {3072, 3072, 12288, 6, false},
         {2560, 2560, 8192, 4, false},   {2560, 2560, 2560, 4, false},   {3584, 3584, 3584, 8, false},
         {4096, 4096, 4096, 8, false},   {4608, 4608, 4608, 4, false},   {5120, 5120, 5120, 8, false},
         {7168, 7168, 7168, 8, false},   {12288, 12288, 12288, 8, false}, {32768, 32768, 32768, 8, false},

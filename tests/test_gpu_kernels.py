@@ -373,6 +373,47 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
+@pytest.mark.parametrize("tail", ["1", "0"])
+@pytest.mark.parametrize("kind", ["f16", "bf16"])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("shape,tile", [((4096, 4352, 1024), "256"), ((3072, 3072, 1024), "128"),
+                                        ((3072, 2816, 1024), "128"), ((7168, 1280, 1088), "256")])
+def test_local_gemm_16bit_tail_split_exact(kind, ta, tb, shape, tile, tail, monkeypatch):
+    """The four-wave kernel's data-parallel rounds + tail (gemm_mfma_h): the
+    last, partly filled round of tiles is a rectangle of C (the last group's
+    last columns) computed as its own GEMM, the full rounds by one launch over
+    the first tiles of the order.  (6144, 4096): 384 256-tiles, the whole last
+    group (8 x 16) the tail; (3072, 3072) in 128-tiles: 576 = 512 + 64, an
+    8 x 8 tail; (3072, 2816): 24 x 22 = 528, 16 tiles rounded up to two group
+    columns; (7168, 1280, 1088): 28 x 5 = 140 256-tiles in one round (no tail),
+    the control.  Exact integer products, tail on and off (ELX_H16_TAIL),
+    bit for bit the same."""
+    monkeypatch.setenv("ELX_H16_TILE", tile)
+    monkeypatch.setenv("ELX_H16_TAIL", tail)
+    m, n, k = shape
+    rng = np.random.default_rng(m + n + k + 7)
+    A = rng.integers(-2, 3, (m, k) if ta == "N" else (k, m)).astype(np.float32)
+    B = rng.integers(-2, 3, (k, n) if tb == "N" else (n, k)).astype(np.float32)
+    C = rng.integers(-64, 65, (m, n)).astype(np.float32)
+    opA = A if ta == "N" else A.T
+    opB = B if tb == "N" else B.T
+    exact = 1.0 * (opA.astype(np.float64) @ opB.astype(np.float64)) - 2.0 * C
+    if kind == "f16":
+        enc = lambda x: np.asfortranarray(x.astype(np.float16))  # noqa: E731
+        fn, want = L.lib().elx_gemm_f16, exact.astype(np.float16).view(np.uint16)
+    else:
+        enc = lambda x: np.asfortranarray(oracle.f32_to_bf16_bits(x))  # noqa: E731
+        fn, want = L.lib().elx_gemm_bf16, oracle.f32_to_bf16_bits(exact.astype(np.float32))
+    dA, dB, dC = dev(enc(A)), dev(enc(B)), dev(enc(C))
+    torch.cuda.synchronize()
+    L.check(fn(OPS[ta], OPS[tb], m, n, k, 1.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0], -2.0,
+               dC.data_ptr(), m, None))
+    sync()
+    got = host(dC, (m, n), np.uint16)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
+
+
 @pytest.mark.parametrize("dt", ["f64", "f32", "bf16", "f16"])
 @pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T")])
 def test_local_gemm_matches_vendor_blas(dt, ta, tb):
