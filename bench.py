@@ -389,7 +389,7 @@ def launch_ranks(argv: list[str], world: int, child_cmd: list[str] | None = None
     import subprocess
     port = _free_port()
     cmd = child_cmd or [sys.executable, "-u", os.path.abspath(__file__)]
-    procs = [subprocess.Popen(cmd + list(argv), env=rank_env(os.environ, r, world, port)) for r in range(world)]
+    procs = []
 
     def stop_all(sig):
         for p in procs:
@@ -402,10 +402,13 @@ def launch_ranks(argv: list[str], world: int, child_cmd: list[str] | None = None
     def on_signal(signum, _frame):
         stop_all(signum)
 
+    # forward SIGTERM / SIGINT from before the first child starts
     old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
     status = 0
     failed_at = None
     try:
+        for r in range(world):
+            procs.append(subprocess.Popen(cmd + list(argv), env=rank_env(os.environ, r, world, port)))
         while True:
             codes = [p.poll() for p in procs]
             for r, c in enumerate(codes):

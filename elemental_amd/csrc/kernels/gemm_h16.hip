@@ -224,7 +224,9 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[M
 // The same loop at half the tile (WM = 4: 128 x 128 per workgroup, 64 x 64 =
 // 4 x 4 accumulators per wave, 80 KiB of ring, two workgroups per CU) serves the
 // grids on which 256 x 256 tiles leave CUs idle (fewer than 256 of them: 2048^3
-// has 64, i.e. a quarter of the chip).  Round 5.
+// has 64, i.e. a quarter of the chip).  Round 5.  Round 6 adds WM = 6 / 5 / 7
+// (192 / 160 / 224 tiles, one workgroup per CU) for grids those edges fill in
+// whole rounds; h16_plan (kernels.hpp) picks the tile.
 //
 // Staging unit = one operand's K-tile image (BM rows x 64 k: 32 KiB at WM = 8,
 // 16 KiB at WM = 4; the KC / RC images: 128-B KC rows, or 256-B RC k-rows in
@@ -265,7 +267,8 @@ template <int WM> struct Geo {
 // per-lane offset (elements from the image's corner at k0) of piece j of one
 // operand's K-tile image, as the image is laid out: KC rows 8j..8j+7 (128 B
 // each); RC k-rows 4(j & 15)..+3 of the 128-column block j >> 4, or, in a
-// 64-column last block (WM = 6), k-rows 8i..8i+7 of it (i = j - 16 RCFULL)
+// 64-column block (WM 6, 7), k-rows 8i..8i+7 of it (i = j - J64), or, in a
+// 32-column block (WM 5, 7), k-rows 16i..16i+15 (i = j - J32)
 template <int WM, bool KC>
 __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld) {
     const int h = j >> 4, ins = j & 15;
@@ -315,8 +318,8 @@ __device__ __forceinline__ void piece(const uint16_t* X, i64 ld, i64 R0, i64 k0,
 }
 
 // a wave's operand fragment f (16 rows) of k-step s: KC images are one block of
-// 128-B rows; RC images are 128-column blocks (and a last 64-column one at
-// WM = 6), so a wave's rows may start inside one
+// 128-B rows; RC images are 128-column blocks (then a 64- and / or a
+// 32-column one, Geo), so a wave's rows may start inside one
 template <int WM, bool KC>
 __device__ __forceinline__ u32x4 wfrag(const lds_char* img, int w_r, int f, int s, int l) {
     constexpr int WR = Geo<WM>::WROWS;

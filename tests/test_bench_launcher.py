@@ -22,6 +22,7 @@ import json, os, sys, time
 d = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                     "MASTER_ADDR", "MASTER_PORT")}
 d["argv"] = sys.argv[1:]
+d["pid"] = os.getpid()
 open(os.path.join(os.environ["OUT_DIR"], "rank%s.json" % d["RANK"]), "w").write(json.dumps(d))
 if d["RANK"] in os.environ.get("FAIL_RANKS", "").split(","):
     sys.exit(3)
@@ -53,6 +54,7 @@ def test_launcher_rank_environment(tmp_path, monkeypatch, capfd):
         assert d["WORLD_SIZE"] == d["LOCAL_WORLD_SIZE"] == "4"
         assert d["MASTER_ADDR"] == "127.0.0.1"
         assert d["argv"] == ["--gpus", "4", "--steps", "3"]
+        assert d["pid"] > 0
     out = capfd.readouterr().out.strip().splitlines()
     assert [json.loads(x) for x in out] == [{"metric": "stand-in", "n_gpus": 4}]
 
@@ -84,3 +86,31 @@ def test_bench_gpus_2_without_launcher_fails_loudly_on_cpu():
     assert p.returncode != 0
     assert "[bench launcher] rank" in p.stderr
     assert p.stdout.strip() == ""
+
+
+def test_launcher_forwards_sigterm(tmp_path):
+    """SIGTERM to the launcher reaches every rank (the driver's timeout ends the
+    whole job, not just the parent): the launcher exits 128 + SIGTERM promptly
+    and no rank survives it."""
+    import signal
+    script = ("import sys; sys.path.insert(0, %r); import bench; "
+              "sys.exit(bench.launch_ranks([], 2, child_cmd=[sys.executable, '-c', %r], grace_s=1.0, poll_s=0.05))"
+              % (ROOT, CHILD))
+    env = dict(os.environ, OUT_DIR=str(tmp_path), SLEEP_S="60")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.Popen([sys.executable, "-c", script], env=env)
+    deadline = time.monotonic() + 60
+    while len(list(tmp_path.glob("rank*.json"))) < 2:  # both ranks started
+        assert time.monotonic() < deadline and p.poll() is None
+        time.sleep(0.05)
+    t0 = time.monotonic()
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    assert time.monotonic() - t0 < 10
+    for f in tmp_path.glob("rank*.json"):
+        pid = json.loads(f.read_text())["pid"]
+        try:  # the rank was reaped by the launcher: no such process
+            os.kill(pid, 0)
+            raise AssertionError(f"rank process {pid} survived the launcher")
+        except ProcessLookupError:
+            pass
