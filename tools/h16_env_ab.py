@@ -2,6 +2,7 @@
 library reads on every call), interleaved so clock drift hits all arms alike.
 
   python tools/h16_env_ab.py VAR v1,v2[,...] [--beta B] [--reps R] dt,ta,tb,m,n,k ...
+  (values that contain commas themselves: separate them with ';', e.g. "2,8;2,4")
 
 Each line: the shape, TFLOP/s per value (best and mean of R interleaved
 rounds, each the best of timeit's repetitions).
@@ -20,7 +21,8 @@ TD = {"f16": torch.float16, "bf16": torch.bfloat16}
 
 def main():
     args = sys.argv[1:]
-    var, vals = args[0], args[1].split(",")
+    var = args[0]
+    vals = args[1].split(";") if ";" in args[1] else args[1].split(",")
     beta, reps, shapes = 1.0, 3, []
     it = iter(args[2:])
     for a in it:
