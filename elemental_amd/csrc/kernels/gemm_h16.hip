@@ -72,6 +72,9 @@ struct H2Params {
     // > 0: launch only the first dp_tiles tiles of the tile order (the
     // data-parallel rounds of gemm_mfma_h's tail split); 0: every tile
     int dp_tiles;
+    // k beyond the last whole K-tile (0..63), added by the workgroup after its
+    // K-tile loop, before the one rounding (split-k: by the last chunk)
+    int ktail;
 };
 
 __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
@@ -298,6 +301,22 @@ __device__ __forceinline__ i64 piece_off(int j, int l, i64 R0, i64 rows, i64 ld)
         const i64 col = R0 + col0 <= rows - 8 ? col0 : rows - 8 - R0;
         return col + kk * ld;
     }
+}
+
+// the same offsets for the k-tail K-tile (ktail < 64 valid k): k-rows (RC) past
+// the tail are clamped to its last one, 16-B k-chunks (KC) past it to chunk 0
+// (with a k-contiguous operand the host takes the in-kernel tail only for
+// ktail % 8 == 0, so no chunk straddles it and nothing is read past k).  The
+// values read for k >= ktail are zeroed in the fragments before use.
+template <int WM, bool KC>
+__device__ __forceinline__ i64 piece_off_tail(int j, int l, i64 R0, i64 rows, i64 ld, int ktail) {
+    const i64 o = piece_off<WM, KC>(j, l, R0, rows, ld);
+    if (KC) {
+        const i64 kin = o % ld;  // 8 c: the chunk's first k
+        return kin < ktail ? o : o - kin;
+    }
+    const i64 kk = o / ld;
+    return kk < ktail ? o : o - (kk - (ktail - 1)) * ld;
 }
 
 template <bool KC>
@@ -578,6 +597,45 @@ __global__ __launch_bounds__(256, WM >= 5 ? 1 : 2) void gemm_h4w_kernel(H2Params
         if (t + 4 < nt) ktile(std::integral_constant<int, 4>{}, t + 4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces
+    // The k tail (< 64 k past the last whole K-tile), in the same accumulators so
+    // C is rounded once: every wave has finished the loop (barrier), the tail's
+    // A and B images go into slots 0 and 1 with k clamped into the tail, and the
+    // fragments' k >= ktail are zeroed before the MFMAs (both operands: what was
+    // read there may be anything).  Outside the loop: the loop is untouched.
+    int ktail = p.ktail;
+    if constexpr (PART) ktail = blockIdx.y + 1 == gridDim.y ? ktail : 0;
+    if (ktail > 0) {
+        bar8();
+        const i64 k0 = (i64)nt * BK;
+#pragma unroll
+        for (int u = 0; u < WM; ++u) {
+            const i64 ga = w4::piece_off_tail<WM, KCA>(w + 4 * u, l, m0, p.m, p.lda, ktail);
+            const i64 gb = w4::piece_off_tail<WM, KCB>(w + 4 * u, l, n0, p.n, p.ldb, ktail);
+            w4::piece<BMR, BUF, KCA>(p.A, p.lda, m0, k0, (int)(ga * 2), ga, w + 4 * u, lds);
+            w4::piece<BMR, BUF, KCB>(p.B, p.ldb, n0, k0, (int)(gb * 2), gb, w + 4 * u, lds + UNIT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar8();
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+            // lane l holds k = 32 sk + 8 (l >> 4) + j, j = 0..7, two per 32-bit word
+            u32x4 mask;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = 32 * sk + 8 * (l >> 4) + 2 * q;
+                mask[q] = (k < ktail ? 0xffffu : 0u) | (k + 1 < ktail ? 0xffff0000u : 0u);
+            }
+            Sets<WM> T;
+#pragma unroll
+            for (int q = 0; q < WM; ++q) {
+                T.a[q] = wfrag<WM, KCA>(lds, wr, q, sk, l) & mask;
+                T.b[q] = wfrag<WM, KCB>(lds + UNIT, wc, q, sk, l) & mask;
+            }
+            asm volatile("s_nop 4" ::: "memory");  // VALU-written operands -> asm MFMA
+#pragma unroll
+            for (int i = 0; i < WM * WM; ++i) w4::mfma_acc<BF16>(acc[i / WM][i % WM], T.a[i / WM], T.b[i % WM]);
+        }
+    }
     w4::settle<WM>(acc);
     if constexpr (PART) w4::epilogue_partial<WM>(p, acc, m0, n0, wr, wc, l);
     else w4::epilogue4<BF16, WM>(p, acc, m0, n0, wr, wc, l);
@@ -687,9 +745,14 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     // (192-tiles measured even to +1 % in the grouped order: 3072^3 NN 1080 ->
     // 1089, 6144^3 1305 -> 1315, profiles/r06c_h16_tile192_sweep.log)
     const int sblock = mode == 1 && pl.wm == 8 && pl.nz == 1 && tm_ % sbr == 0 && tn_ % sbc == 0;
+    // the k tail goes into the kernel (one rounding of C) unless a k-contiguous
+    // operand would need a 16-B chunk straddling k (k % 8 != 0): then a second
+    // pass adds it to the rounded C (ELX_H16_KTAIL = 0 forces that, for A/B)
+    const char* kt_env = getenv("ELX_H16_KTAIL");
+    const bool tail_in = kmain != k && !(kt_env && kt_env[0] == '0') && (!(kca || kcb) || k % 8 == 0);
     H2Params p{m, n, kmain, alpha, beta, A, lda, B, ldb, C, ldc, tm_, tn_,
                (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0, GroupM(), sblock, xr, pr, pl.kchunk,
-               nullptr, 0};
+               nullptr, 0, tail_in ? (int)(k - kmain) : 0};
     const i64 nz = pl.nz;
     hipError_t e;
     auto launch = [&]() {
@@ -721,7 +784,7 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     const char* tv = getenv("ELX_H16_TAIL");
     const bool tail_on = !(tv && tv[0] == '0');
     const i64 slots = pl.wm == 4 ? 512 : 256;
-    if (tail_on && nz == 1 && !sblock && kmain == k && k >= 1024 && tiles > slots) {
+    if (tail_on && nz == 1 && !sblock && (kmain == k || tail_in) && k >= 1024 && tiles > slots) {
         const i64 rem = tiles % slots;
         const int G = p.group_m;
         const int last = (tm_ - 1) / G, gsz = tm_ - last * G;  // the last group's tile rows
@@ -755,8 +818,8 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
         const hipError_t f = workspace_free(p.W, s);
         if (e == hipSuccess) e = f;
     }
-    if (e != hipSuccess || kmain == k) return e;
-    // k tail (< 64): C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
+    if (e != hipSuccess || kmain == k || tail_in) return e;
+    // k tail (< 64) as a second pass: C += alpha op(A)(:, kmain:) op(B)(kmain:, :)
     const uint16_t* At = ta ? A + kmain : A + kmain * lda;
     const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
     return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);

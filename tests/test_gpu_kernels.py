@@ -323,7 +323,8 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
 @pytest.mark.parametrize("tb", ["N", "T"])
 @pytest.mark.parametrize("shape", [(2048, 2312, 2112), (4096, 2048, 640), (2304, 2048, 64), (1024, 1024, 8192),
                                    (1002, 1032, 4096), (2048, 2048, 2112), (1536, 2312, 704), (4096, 4096, 192),
-                                   (3072, 3072, 192), (2560, 2560, 192), (3584, 3584, 128)])
+                                   (3072, 3072, 192), (2560, 2560, 192), (3584, 3584, 128), (2048, 2312, 2088),
+                                   (1536, 2312, 712)])
 def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     """Integer operands in [-2, 2]: every partial sum is exact in the f32
     accumulators, so alpha op(A) op(B) + beta C is exact before the one rounding
@@ -341,8 +342,9 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     a 32-column block: 192 = 128 + 64, 160 = 128 + 32, 224 = 128 + 64 + 32).
     (4096, 4096, 192) / (3072, 3072, 192) / (2560, 2560, 192) / (3584, 3584,
     128): 16 x 16 grids of 256- / 192- / 160- / 224-tiles (the 256-tiles' in the
-    super-block tile order, tile_of_sb).  (k a multiple of 64: a k tail is a
-    second pass that adds to the already rounded C.)  tile = "g": the plan's
+    super-block tile order, tile_of_sb).  (2048, 2312, 2088) / (1536, 2312, 712):
+    a k tail of 40 / 8 past the last whole K-tile, added inside the kernel
+    before the one rounding.  tile = "g": the plan's
     tile with the DMA in its 64-bit-address form (ELX_H16_STAGE=g; operands too
     long for 31-bit buffer offsets take it)."""
     if tile == "g":
@@ -371,6 +373,45 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     got = host(dC, (m, n), np.uint16)
     bad = np.argwhere(got != want)
     assert bad.size == 0, f"{kind} {ta}{tb}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
+
+
+@pytest.mark.parametrize("kind", ["f16", "bf16"])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
+@pytest.mark.parametrize("k", [2088, 4104, 1091, 2047])
+def test_local_gemm_16bit_ktail_rounding(kind, ta, tb, k):
+    """k not a multiple of 64.  With both operands rows-contiguous (NT) the tail
+    is always added inside the kernel, so C is rounded once: bit-exact.  With a
+    k-contiguous operand that needs k % 8 == 0 (whole 16-B chunks); otherwise
+    (1091, 2047) the tail is a second pass over the rounded C: bf16 within one
+    ulp of the exact rounding (f16 holds these integers exactly).  2088 / 4104:
+    tails of 40 / 8 with k % 8 == 0, in the kernel in every orientation."""
+    m, n = 2048, 2312
+    rng = np.random.default_rng(m + n + k)
+    A = rng.integers(-2, 3, (m, k) if ta == "N" else (k, m)).astype(np.float32)
+    B = rng.integers(-2, 3, (k, n) if tb == "N" else (n, k)).astype(np.float32)
+    C = rng.integers(-64, 65, (m, n)).astype(np.float32)
+    opA = A if ta == "N" else A.T
+    opB = B if tb == "N" else B.T
+    exact = 1.0 * (opA.astype(np.float64) @ opB.astype(np.float64)) - 2.0 * C
+    if kind == "f16":
+        enc = lambda x: np.asfortranarray(x.astype(np.float16))  # noqa: E731
+        fn, want = L.lib().elx_gemm_f16, exact.astype(np.float16).view(np.uint16)
+    else:
+        enc = lambda x: np.asfortranarray(oracle.f32_to_bf16_bits(x))  # noqa: E731
+        fn, want = L.lib().elx_gemm_bf16, oracle.f32_to_bf16_bits(exact.astype(np.float32))
+    dA, dB, dC = dev(enc(A)), dev(enc(B)), dev(enc(C))
+    torch.cuda.synchronize()
+    L.check(fn(OPS[ta], OPS[tb], m, n, k, 1.0, dA.data_ptr(), A.shape[0], dB.data_ptr(), B.shape[0], -2.0,
+               dC.data_ptr(), m, None))
+    sync()
+    got = host(dC, (m, n), np.uint16)
+    in_kernel = (ta == "N" and tb == "T") or k % 8 == 0
+    if in_kernel or kind == "f16":
+        bad = np.argwhere(got != want)
+        assert bad.size == 0, f"{kind} {ta}{tb} k={k}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
+    else:  # two roundings: at most one bf16 ulp from the exact rounding (same sign, adjacent codes)
+        d = np.abs(got.astype(np.int32) - want.astype(np.int32))
+        assert d.max() <= 1, (kind, ta, tb, k, int(d.max()))
 
 
 @pytest.mark.parametrize("tail", ["1", "0"])

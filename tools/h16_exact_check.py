@@ -7,7 +7,8 @@ Integer operands in [-2, 2]: every partial sum is exact in f32, so the result
 must equal numpy's rounding of the exact value bit for bit (as
 tests/test_gpu_kernels.py::test_local_gemm_16bit_exact), all four orientations,
 bf16 and f16.  Prints one line per case and exits non-zero on any mismatch.
-Exact only for k a multiple of 64: a k tail is a second pass that adds to the
+Exact for every k whose tail the kernel takes itself (k % 8 == 0, or both
+operands rows-contiguous); otherwise a second pass adds the tail to the
 already rounded C ("Exactness and the k tail").
 """
 import os
