@@ -706,11 +706,24 @@ int GroupM() {
 // Tile size and split-k of the four-wave kernel: h16_plan in kernels.hpp.
 
 #ifndef ELX_KERNEL_PROBE
+namespace {
+hipError_t gemm_mfma_h_plan(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
+                            i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s,
+                            const H16Plan* forced);
+}
+
 hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
                        i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s) {
+    return gemm_mfma_h_plan(is_bf16, ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s, nullptr);
+}
+
+namespace {
+hipError_t gemm_mfma_h_plan(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, float alpha, const uint16_t* A,
+                            i64 lda, const uint16_t* B, i64 ldb, float beta, uint16_t* C, i64 ldc, hipStream_t s,
+                            const H16Plan* forced) {
     const bool kca = ta, kcb = !tb;
     const i64 kmain = k / BK * BK;
-    const H16Plan pl = h16_plan(m, n, kmain, kca && kcb);
+    const H16Plan pl = forced ? *forced : h16_plan(m, n, kmain, kca && kcb);
     const int BMR = pl.wm * 32;
     const i64 tiles = ((m + BMR - 1) / BMR) * ((n + BMR - 1) / BMR);
     // the LDS-DMA path: 16-B aligned rows/columns for the DMA, RC operands a
@@ -779,23 +792,53 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     // 64) 1322 -> 1375 (1280), 6144^3 in 256-tiles (576 = 2 x 256 + 64) 1231 ->
     // 1290 (1285), TN 1263 -> 1328, 3072^2 x 4096 in 128-tiles (576 = 512 + 64)
     // 864 -> 904; a last round of half the slots lost (6144 x 4096^2, 384 =
-    // 256 + 128: 1193 -> 1167), hence the quarter.  ELX_H16_TAIL = 0 turns it
-    // off (read per call, for A/B).
+    // 256 + 128: 1193 -> 1167), hence the quarter.  A last round of 256-tiles
+    // a quarter to a third full (not TN) runs as split-k over the same tiles
+    // instead, z = 256 / tiles >= 3 chunks of k each (f32 partials, one
+    // reduce): in one process against the 256-tile grid and the plan without
+    // it (profiles/r06v_h16_tailsk_ab.log, beta 0): 4608^3 (324 = 256 + 68)
+    // NN 994 / 1042 -> 1107 TF, NT 966 / 1026 -> 1086, f16 NN 991 / 986 ->
+    // 1078; TN's 224-tiles stay ahead (1160 vs 1129), and at half a round the
+    // split loses (6144 x 4096^2: 1105 vs 1156), hence z >= 3.  The group
+    // height shrinks (8 -> 6 at 4608^3) where the last group holds fewer tiles
+    // than the tail.  ELX_H16_TAIL = 0 turns both off, ELX_H16_TAILSK = 0 the
+    // split-k form (read per call, for A/B).
     const char* tv = getenv("ELX_H16_TAIL");
-    const bool tail_on = !(tv && tv[0] == '0');
+    const bool tail_on = !(tv && tv[0] == '0') && !forced;
     const i64 slots = pl.wm == 4 ? 512 : 256;
     if (tail_on && nz == 1 && !sblock && (kmain == k || tail_in) && k >= 1024 && tiles > slots) {
         const i64 rem = tiles % slots;
-        const int G = p.group_m;
+        // split-k tail: see h16_plan; ELX_H16_TAILSK = 0 turns it off (per call)
+        const char* skv = getenv("ELX_H16_TAILSK");
+        const bool tail_sk = !(skv && skv[0] == '0') && pl.wm == 8 && !(kca && kcb) && rem > slots / 4 &&
+                             3 * rem <= slots;
+        // the group height whose last group holds the whole tail (G = 8 unless
+        // the last group is shorter than the tail)
+        int G = p.group_m;
+        for (int g = G; g >= 2; --g) {
+            const int gs = tm_ - (tm_ - 1) / g * g;
+            if ((i64)gs * tn_ >= rem) { G = g; break; }
+        }
         const int last = (tm_ - 1) / G, gsz = tm_ - last * G;  // the last group's tile rows
         const i64 cols = (rem + gsz - 1) / gsz;                 // its tail columns
-        if (rem > 0 && rem <= slots / 4 && cols <= tn_) {
+        if (rem > 0 && (rem <= slots / 4 || tail_sk) && cols <= tn_) {
+            p.group_m = G;
             p.dp_tiles = (int)(tiles - cols * gsz);
             e = launch();
             if (e != hipSuccess) return e;
             const i64 i0 = (i64)last * G * BMR, j0 = (tn_ - cols) * BMR;
-            return gemm_mfma_h(is_bf16, ta, tb, m - i0, n - j0, k, alpha, ta ? A + i0 * lda : A + i0, lda,
-                               tb ? B + j0 : B + j0 * ldb, ldb, beta, C + i0 + j0 * ldc, ldc, s);
+            const uint16_t* At = ta ? A + i0 * lda : A + i0;
+            const uint16_t* Bt = tb ? B + j0 : B + j0 * ldb;
+            if (!tail_sk)
+                return gemm_mfma_h(is_bf16, ta, tb, m - i0, n - j0, k, alpha, At, lda, Bt, ldb, beta, C + i0 + j0 * ldc,
+                                   ldc, s);
+            // split-k tail: the same tiles, each over z >= 3 chunks of k, z = slots / tiles
+            H16Plan tp = pl;
+            const i64 z = std::max<i64>(1, slots / (cols * gsz));
+            tp.kchunk = ((kmain + z - 1) / z + BK - 1) / BK * BK;
+            tp.nz = (kmain + tp.kchunk - 1) / tp.kchunk;
+            return gemm_mfma_h_plan(is_bf16, ta, tb, m - i0, n - j0, k, alpha, At, lda, Bt, ldb, beta,
+                                    C + i0 + j0 * ldc, ldc, s, &tp);
         }
     }
     if (nz > 1) {
@@ -824,6 +867,7 @@ hipError_t gemm_mfma_h(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k, floa
     const uint16_t* Bt = tb ? B + kmain * ldb : B + kmain;
     return gemm_mfma_h_simple(is_bf16, ta, tb, m, n, k - kmain, alpha, At, lda, Bt, ldb, 1.0f, C, ldc, s);
 }
+}  // namespace
 
 #endif  // ELX_KERNEL_PROBE
 

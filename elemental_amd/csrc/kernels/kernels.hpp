@@ -130,7 +130,9 @@ struct H16Plan { int wm; i64 nz, kchunk; };
 //    bytes per FLOP than the 256-tile).  A grid whose last round of 256-tiles
 //    is at most a quarter full counts as 0.95: gemm_mfma_h's tail split runs
 //    that round on smaller tiles (6144^3: 256-tiles with the tail 1290 TF, the
-//    192-tiles 1185 on the same box, profiles/r06j_h16_tail_split_ab.log).  Below 128 256-tiles the 128-tiles
+//    192-tiles 1185 on the same box, profiles/r06j_h16_tail_split_ab.log); one
+//    a quarter to a third full (not TN) as 0.9: the tail runs split-k (4608^3 NN
+//    1107 TF against 1042 on 128-tiles, profiles/r06v_h16_tailsk_ab.log).  Below 128 256-tiles the 128-tiles
 //    stay (2560^3: 128-tiles 856 / 880 against 834 / 710 for 192), except for
 //    TN grids of nearly a full round of 160-tiles (below).
 //  * TN (both operands k-contiguous) may also take 224 x 224 (WM = 7) and
@@ -157,9 +159,13 @@ inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
         // a separate GEMM on smaller tiles (the tail split): such a grid counts
         // as nearly full
         const char* tl = getenv("ELX_H16_TAIL");
+        const char* sk = getenv("ELX_H16_TAILSK");
         const i64 t8 = tiles_of(256), r8 = t8 % 256;
-        const bool tail8 = !(tl && tl[0] == '0') && t8 > 256 && r8 > 0 && r8 <= 64 && kmain >= 1024;
-        const double u8 = tail8 ? 0.95 : util(t8, 256);
+        const bool tail_ok = !(tl && tl[0] == '0') && t8 > 256 && kmain >= 1024;
+        const bool tail8 = tail_ok && r8 > 0 && r8 <= 64;
+        // a quarter to a third of a round: the split-k tail (not TN)
+        const bool sk8 = tail_ok && !tn && !(sk && sk[0] == '0') && r8 > 64 && 3 * r8 <= 256;
+        const double u8 = tail8 ? 0.95 : sk8 ? 0.9 : util(t8, 256);
         pl.wm = 8;
         if (u8 <= 0.75) {
             double best = u8;

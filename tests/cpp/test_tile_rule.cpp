@@ -46,18 +46,21 @@ int main() {
     const elx::kern::DmaPlan t64 = elx::kern::dma_plan(true, 256, 2048, 16);  // 1024^2 in 64-tiles
     if (!t64.use || t64.nz != 1) { std::printf("FAIL plan 256 tiles: nz %d\n", t64.nz); ++bad; }
     // the 16-bit four-wave kernel's tile (h16_plan): 256 / 192 / 128 by the
-    // round-6 map (profiles/r06d_h16_tile_map.log, r06c_h16_tile192_sweep.log)
+    // round-6 map (profiles/r06d_h16_tile_map.log, r06c_h16_tile192_sweep.log);
+    // 4608^3 (324 256-tiles) takes 256 with the split-k tail, TN the 224-tiles
+    // (profiles/r06v_h16_tailsk_ab.log)
     struct H { i64 m, n, k; int wm; bool tn; };
     const H hc[] = {
         {3072, 3072, 3072, 6, false},   {6144, 6144, 6144, 8, false},   {3072, 3072, 12288, 6, false},
         {2560, 2560, 8192, 4, false},   {2560, 2560, 2560, 4, false},   {3584, 3584, 3584, 8, false},
-        {4096, 4096, 4096, 8, false},   {4608, 4608, 4608, 4, false},   {5120, 5120, 5120, 8, false},
+        {4096, 4096, 4096, 8, false},   {4608, 4608, 4608, 8, false},   {5120, 5120, 5120, 8, false},
         {7168, 7168, 7168, 8, false},   {12288, 12288, 12288, 8, false}, {32768, 32768, 32768, 8, false},
         {16384, 8192, 8192, 8, false},  {2048, 2048, 2048, 4, false},   {1536, 2048, 2048, 4, false},
         {1024, 1024, 8192, 4, false},   {4096, 2048, 4096, 4, false},   {8192, 4096, 2048, 8, false},
         // TN may take the 224- and 160-tiles
         {3584, 3584, 3584, 7, true},    {2560, 2560, 2560, 5, true},    {3072, 3072, 3072, 6, true},
         {4096, 4096, 4096, 8, true},    {16384, 16384, 16384, 8, true}, {2048, 2048, 2048, 4, true},
+        {4608, 4608, 4608, 7, true},
     };
     for (const H& c : hc) {
         const elx::kern::H16Plan pl = elx::kern::h16_plan(c.m, c.n, c.k, c.tn);

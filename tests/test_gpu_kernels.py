@@ -418,7 +418,8 @@ def test_local_gemm_16bit_ktail_rounding(kind, ta, tb, k):
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T")])
 @pytest.mark.parametrize("shape,tile", [((4096, 4352, 1024), "256"), ((3072, 3072, 1024), "128"),
-                                        ((3072, 2816, 1024), "128"), ((7168, 1280, 1088), "256")])
+                                        ((3072, 2816, 1024), "128"), ((7168, 1280, 1088), "256"),
+                                        ((4608, 4608, 1024), "256"), ((4608, 4608, 1064), "256")])
 def test_local_gemm_16bit_tail_split_exact(kind, ta, tb, shape, tile, tail, monkeypatch):
     """The four-wave kernel's data-parallel rounds + tail (gemm_mfma_h): the
     last, partly filled round of tiles is a rectangle of C (the last group's
@@ -427,8 +428,12 @@ def test_local_gemm_16bit_tail_split_exact(kind, ta, tb, shape, tile, tail, monk
     group (8 x 16) the tail; (3072, 3072) in 128-tiles: 576 = 512 + 64, an
     8 x 8 tail; (3072, 2816): 24 x 22 = 528, 16 tiles rounded up to two group
     columns; (7168, 1280, 1088): 28 x 5 = 140 256-tiles in one round (no tail),
-    the control.  Exact integer products, tail on and off (ELX_H16_TAIL),
-    bit for bit the same."""
+    the control; (4608, 4608): 324 = 256 + 68 256-tiles, a tail between a
+    quarter and a third of a round, run as split-k over the same tiles (the
+    group height shrinks to 6 so the last group holds it; z = 3 chunks of k,
+    and with k = 1064 the last chunk also takes the 40-deep k tail; TN keeps
+    the smaller-tile form: no split-k tail there).  Exact integer products, tail
+    on and off (ELX_H16_TAIL), bit for bit the same."""
     monkeypatch.setenv("ELX_H16_TILE", tile)
     monkeypatch.setenv("ELX_H16_TAIL", tail)
     m, n, k = shape
