@@ -420,6 +420,36 @@ __global__ __launch_bounds__(256) void h16_splitk_reduce(i64 m, i64 n, int nz, f
     }
 }
 
+// The same sum, four rows of one column per thread (16-B partial loads, 8-B C
+// accesses; m % 4 == 0, C 8-B aligned, ldc % 4 == 0): grid (ceil(m / 1024), n).
+// Same order of additions (W_0 + W_1 + ...), so the same bits.
+template <bool BF16>
+__global__ __launch_bounds__(256) void h16_splitk_reduce4(i64 m, i64 n, int nz, float alpha,
+                                                          const float* __restrict__ W, float beta,
+                                                          uint16_t* __restrict__ C, i64 ldc) {
+    using E = typename std::conditional<BF16, Elem<bf16_t>, Elem<f16_t>>::type;
+    const i64 i = ((i64)blockIdx.x * 256 + threadIdx.x) * 4, j = blockIdx.y;
+    if (i >= m) return;
+    const i64 mn = m * n;
+    const float* w = W + j * m + i;
+    f32x4 v = *reinterpret_cast<const f32x4*>(w);
+    for (int z = 1; z < nz; ++z) v += *reinterpret_cast<const f32x4*>(w + z * mn);
+    uint16_t* o = C + i + j * ldc;
+    uint2 cv = make_uint2(0, 0);
+    if (beta != 0.f) cv = *reinterpret_cast<const uint2*>(o);
+    const uint16_t in[4] = {(uint16_t)(cv.x & 0xffff), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xffff),
+                            (uint16_t)(cv.y >> 16)};
+    uint16_t r16[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float x = v[r] * alpha;
+        if (beta != 0.f) x += beta * E::load(in[r]);
+        r16[r] = E::store(x);
+    }
+    *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)r16[0] | ((uint32_t)r16[1] << 16),
+                                              (uint32_t)r16[2] | ((uint32_t)r16[3] << 16));
+}
+
 // C tile of one wave (16 WM x 16 WM): accumulator (mi, ni) holds rows
 // rb + 16 mi + 4 (l >> 4) + {0..3}, column cb + 16 ni + (l & 15).  One row of
 // accumulators at a time (C loads, then stores), so at most 4 WM values live in
@@ -847,7 +877,19 @@ hipError_t gemm_mfma_h_plan(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k,
     }
     e = launch();
     if (nz > 1) {
-        if (e == hipSuccess) {
+        const char* rv = getenv("ELX_H16_RED");
+        const bool red4 = !(rv && rv[0] == '0') && m % 4 == 0 && n <= 65535 &&
+                          (reinterpret_cast<uintptr_t>(C) & 7) == 0 && ldc % 4 == 0;
+        if (e == hipSuccess && red4) {
+            const dim3 grid((unsigned)((m + 1023) / 1024), (unsigned)n);
+            if (is_bf16)
+                hipLaunchKernelGGL((w4::h16_splitk_reduce4<true>), grid, dim3(256), 0, s, m, n, (int)nz, alpha, p.W,
+                                   beta, C, ldc);
+            else
+                hipLaunchKernelGGL((w4::h16_splitk_reduce4<false>), grid, dim3(256), 0, s, m, n, (int)nz, alpha, p.W,
+                                   beta, C, ldc);
+            e = hipGetLastError();
+        } else if (e == hipSuccess) {
             const i64 mn = m * n;
             const unsigned grid = (unsigned)std::min<i64>((mn + 255) / 256, 2048);
             if (is_bf16)
