@@ -132,7 +132,12 @@ struct H16Plan { int wm; i64 nz, kchunk; };
 //    that round on smaller tiles (6144^3: 256-tiles with the tail 1290 TF, the
 //    192-tiles 1185 on the same box, profiles/r06j_h16_tail_split_ab.log); one
 //    a quarter to a third full (not TN) as 0.9: the tail runs split-k (4608^3 NN
-//    1107 TF against 1042 on 128-tiles, profiles/r06v_h16_tailsk_ab.log).  Below 128 256-tiles the 128-tiles
+//    1107 TF against 1042 on 128-tiles, profiles/r06v_h16_tailsk_ab.log).  At
+//    exactly 0.75 (1.5 rounds: 6144 x 4096, 3072 x 8192) the 256-tiles stay:
+//    the half-filled round runs at a higher clock than its share predicts
+//    (bf16 NN 6144 x 4096 x 8192 1273 vs 1087 TF on 128-tiles, x 4096 1116 vs
+//    1108 at beta 1 and 1182 vs 1139 at beta 0, f16 1148 vs 1128; NT 1084 vs
+//    1099; profiles/r06y_h16_t384_ab.log).  Below 128 256-tiles the 128-tiles
 //    stay (2560^3: 128-tiles 856 / 880 against 834 / 710 for 192), except for
 //    TN grids of nearly a full round of 160-tiles (below).
 //  * TN (both operands k-contiguous) may also take 224 x 224 (WM = 7) and
@@ -167,7 +172,7 @@ inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
         const bool sk8 = tail_ok && !tn && !(sk && sk[0] == '0') && r8 > 64 && 3 * r8 <= 256;
         const double u8 = tail8 ? 0.95 : sk8 ? 0.9 : util(t8, 256);
         pl.wm = 8;
-        if (u8 <= 0.75) {
+        if (u8 < 0.75) {
             double best = u8;
             const double s6 = 0.8 * util(tiles_of(192), 256), s4 = 0.8 * util(tiles_of(128), 512);
             if (s6 > best) { best = s6; pl.wm = 6; }
