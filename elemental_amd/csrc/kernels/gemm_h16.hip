@@ -229,7 +229,9 @@ __device__ __forceinline__ void epilogue(const H2Params& p, const f32x4 (&acc)[M
 // grids on which 256 x 256 tiles leave CUs idle (fewer than 256 of them: 2048^3
 // has 64, i.e. a quarter of the chip).  Round 5.  Round 6 adds WM = 6 / 5 / 7
 // (192 / 160 / 224 tiles, one workgroup per CU) for grids those edges fill in
-// whole rounds; h16_plan (kernels.hpp) picks the tile.
+// whole rounds, and WM = 2 (64 x 64, 2 x 2 accumulators per wave, 40 KiB of
+// ring, four workgroups per CU) for small grids; h16_plan (kernels.hpp) picks
+// the tile.
 //
 // Staging unit = one operand's K-tile image (BM rows x 64 k: 32 KiB at WM = 8,
 // 16 KiB at WM = 4; the KC / RC images: 128-B KC rows, or 256-B RC k-rows in
@@ -536,7 +538,7 @@ __device__ __forceinline__ void kstep(const H2Params& p, i64 m0, i64 n0, int w, 
 // SWP: B is the operand of the even units (staged first in a K-tile, one k-step
 // more DMA lead), A of the odd ones.
 template <int WM, bool BF16, bool KCA, bool KCB, bool BUF, bool PART, bool SWP = false>
-__global__ __launch_bounds__(256, WM >= 5 ? 1 : 2) void gemm_h4w_kernel(H2Params p) {
+__global__ __launch_bounds__(256, WM >= 5 ? 1 : WM >= 4 ? 2 : 4) void gemm_h4w_kernel(H2Params p) {
     using namespace w4;
     constexpr int BMR = Geo<WM>::BM, UNIT = Geo<WM>::UNIT;
     __shared__ __attribute__((aligned(1024))) char lds_raw[NSLOT * UNIT];
@@ -804,6 +806,7 @@ hipError_t gemm_mfma_h_plan(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k,
         case 7: return launch_h16_all<7>(is_bf16, kca, kcb, p, s);
         case 6: return launch_h16_all<6>(is_bf16, kca, kcb, p, s);
         case 5: return launch_h16_all<5>(is_bf16, kca, kcb, p, s);
+        case 2: return launch_h16_all<2>(is_bf16, kca, kcb, p, s);
         default: return launch_h16_all<4>(is_bf16, kca, kcb, p, s);
         }
     };
@@ -835,7 +838,7 @@ hipError_t gemm_mfma_h_plan(bool is_bf16, bool ta, bool tb, i64 m, i64 n, i64 k,
     // split-k form (read per call, for A/B).
     const char* tv = getenv("ELX_H16_TAIL");
     const bool tail_on = !(tv && tv[0] == '0') && !forced;
-    const i64 slots = pl.wm == 4 ? 512 : 256;
+    const i64 slots = pl.wm == 4 ? 512 : pl.wm == 2 ? 1024 : 256;
     if (tail_on && nz == 1 && !sblock && (kmain == k || tail_in) && k >= 1024 && tiles > slots) {
         const i64 rem = tiles % slots;
         // split-k tail: see h16_plan; ELX_H16_TAILSK = 0 turns it off (per call)

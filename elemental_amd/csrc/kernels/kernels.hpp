@@ -146,7 +146,15 @@ struct H16Plan { int wm; i64 nz, kchunk; };
 //    (980).  With a rows-contiguous operand they lose (NN 3584^3 224-tiles 1074
 //    vs 1181: their last RC block is 32 columns, 64-B k-rows, twice the DMA
 //    requests per byte of the 128-column blocks), so other orientations never
-//    take them.  ELX_H16_TILE = 256 / 224 / 192 / 160 / 128 forces one (read per
+//    take them.
+//  * 64 x 64 tiles (WM = 2, four workgroups per CU) where 64 to 255 128-tiles
+//    leave CUs idle and k is too short to split: in one process at beta 1
+//    (profiles/r06z2_h16_t64_ab.log, bf16, 128 -> 64): 1024^3 175 -> 290 TF,
+//    1024 x 2048 x 1024 340 -> 474, 2048 x 1024 x 4096 431 -> 570, 1536^3 359
+//    -> 417, 1536 x 2048^2 522 -> 549; at 256 128-tiles and above the 128-tiles
+//    win (2048^3 674 vs 580, 2560^3 805 vs 538), and split-k beats them where k
+//    is long (1024^2 x 8192 490 vs 374).  ELX_H16_TILE = 256 / 224 / 192 / 160 /
+//    128 / 64 forces one (read per
 //    call, for A/B).
 inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
     constexpr i64 BK = 64;  // the four-wave kernel's K-tile
@@ -155,10 +163,17 @@ inline H16Plan h16_plan(i64 m, i64 n, i64 kmain, bool tn = false) {
     auto tiles_of = [&](i64 bm) { return ((m + bm - 1) / bm) * ((n + bm - 1) / bm); };
     auto util = [](i64 t, i64 slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
     H16Plan pl;
-    if (force == 128 || force == 160 || force == 192 || force == 224 || force == 256) {
+    if (force == 64 || force == 128 || force == 160 || force == 192 || force == 224 || force == 256) {
         pl.wm = force / 32;
     } else if (tiles_of(256) < 128) {
         pl.wm = tn && tiles_of(160) >= 224 ? 5 : 4;
+        // 64 x 64 tiles (four workgroups per CU) where the 128-tiles fill fewer
+        // than one CU each and would not split k
+        const i64 t4 = tiles_of(128);
+        if (pl.wm == 4 && t4 >= 64 && t4 < 256) {
+            const i64 z4 = t4 <= 64 && kmain >= 8 * BK ? std::min<i64>((256 + t4 - 1) / t4, kmain / (16 * BK)) : 1;
+            if (z4 < 2) pl.wm = 2;
+        }
     } else {
         // gemm_mfma_h runs a last round of at most a quarter of the slots as
         // a separate GEMM on smaller tiles (the tail split): such a grid counts

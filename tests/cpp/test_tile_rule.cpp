@@ -55,9 +55,12 @@ int main() {
         {2560, 2560, 8192, 4, false},   {2560, 2560, 2560, 4, false},   {3584, 3584, 3584, 8, false},
         {4096, 4096, 4096, 8, false},   {4608, 4608, 4608, 8, false},   {5120, 5120, 5120, 8, false},
         {7168, 7168, 7168, 8, false},   {12288, 12288, 12288, 8, false}, {32768, 32768, 32768, 8, false},
-        {16384, 8192, 8192, 8, false},  {2048, 2048, 2048, 4, false},   {1536, 2048, 2048, 4, false},
+        {16384, 8192, 8192, 8, false},  {2048, 2048, 2048, 4, false},   {1536, 2048, 2048, 2, false},
         {1024, 1024, 8192, 4, false},   {4096, 2048, 4096, 4, false},   {8192, 4096, 2048, 8, false},
         {6144, 4096, 4096, 8, false},   {3072, 8192, 4096, 8, false},   // 1.5 rounds: 256 stays
+        // 64-tiles: 64..255 128-tiles and no split-k
+        {1024, 1024, 1024, 2, false},   {1536, 1536, 1536, 2, false},   {1024, 2048, 1024, 2, false},
+        {512, 1024, 1024, 4, false},    {1024, 1024, 1024, 2, true},
         // TN may take the 224- and 160-tiles
         {3584, 3584, 3584, 7, true},    {2560, 2560, 2560, 5, true},    {3072, 3072, 3072, 6, true},
         {4096, 4096, 4096, 8, true},    {16384, 16384, 16384, 8, true}, {2048, 2048, 2048, 4, true},

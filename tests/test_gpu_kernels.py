@@ -317,7 +317,7 @@ def test_local_gemm_16bit_split_alpha_beta_exact(kind, alpha, beta):
     assert bad.size == 0, f"{kind} alpha={alpha} beta={beta}: {len(bad)} mismatches, first at {bad[:4].tolist()}"
 
 
-@pytest.mark.parametrize("tile", ["", "128", "160", "192", "224", "256", "g"])
+@pytest.mark.parametrize("tile", ["", "64", "128", "160", "192", "224", "256", "g"])
 @pytest.mark.parametrize("kind", ["f16", "bf16"])
 @pytest.mark.parametrize("ta", ["N", "T"])
 @pytest.mark.parametrize("tb", ["N", "T"])
@@ -337,7 +337,7 @@ def test_local_gemm_16bit_exact(kind, ta, tb, shape, tile, monkeypatch):
     tiles, (1024, 1024, 8192) 16, (1002, 1032, 4096) 13 with m % 4 != 0 (the
     partials' scalar stores; TN / TT only, the others take the simple kernel).
     `tile`: the four-wave kernel's tile as the plan picks it (""), or forced to
-    128 / 160 / 192 / 224 / 256 (ELX_H16_TILE), so every instantiation sees
+    64 / 128 / 160 / 192 / 224 / 256 (ELX_H16_TILE), so every instantiation sees
     every shape (rows-contiguous images in 128-column blocks plus a 64- and / or
     a 32-column block: 192 = 128 + 64, 160 = 128 + 32, 224 = 128 + 64 + 32).
     (4096, 4096, 192) / (3072, 3072, 192) / (2560, 2560, 192) / (3584, 3584,
